@@ -1,0 +1,486 @@
+// C ABI (include/gpmpc_mi355x.h): handle management, GP upload, batched control step.
+#include "../../include/gpmpc_mi355x.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gpmpc_common.h"
+
+using namespace gpmpc;
+
+namespace {
+thread_local std::string g_err;
+
+gpmpc_status fail(gpmpc_status s, const std::string& msg) {
+    g_err = msg;
+    return s;
+}
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(GPMPC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+struct ModelDims {
+    int nx, nu, ngp, nparams;
+    int gp_dim[kMaxGP];
+    int var_src[kMaxGP][3];
+};
+
+bool model_dims(int id, ModelDims& m) {
+    switch (id) {
+        case kQuad2D:
+            m = ModelDims{6, 2, 2, 6, {1, 3, 0, 0}, {{6, 0, 0}, {4, 5, 7}, {0, 0, 0}, {0, 0, 0}}};
+            return true;
+        case kQuad3D:
+            m = ModelDims{12, 4, 3, 9, {1, 3, 3, 0}, {{0, 0, 0}, {1, 2, 3}, {4, 5, 6}, {0, 0, 0}}};
+            return true;
+        case kCartpole:
+            m = ModelDims{4, 1, 2, 4, {3, 3, 0, 0}, {{2, 3, 4}, {2, 3, 4}, {0, 0, 0}, {0, 0, 0}}};
+            return true;
+    }
+    return false;
+}
+}  // namespace
+
+struct gpmpc_handle {
+    int device = 0;
+    int model = 0;
+    int H = 0;
+    int max_batch = 0;
+    ModelDims md{};
+    int nb = 0;
+    bool model_set = false, ref_set = false;
+    bool gp_set[kMaxGP] = {false, false, false, false};
+    bool any_prev = false;
+    ProblemDev P{};
+    // device state
+    double *x = nullptr, *u = nullptr, *pi = nullptr, *lam = nullptr, *var = nullptr, *tight = nullptr;
+    int32_t* has_prev = nullptr;
+    double* traj = nullptr;
+    double* plant_params = nullptr;
+    double plant_params_host[kMaxParams] = {0};
+    bool plant_params_valid = false;
+    double* gp_rows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
+    double* gp_vrows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
+    double* gp_linvT[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
+    int gp_npad[kMaxGP] = {0, 0, 0, 0};
+    int32_t* scratch_i = nullptr;   // [2][max_batch]
+    double* scratch_d = nullptr;    // [max_batch][4]
+};
+
+static void free_handle(gpmpc_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params})
+        if (p) (void)hipFree(p);
+    if (h->has_prev) (void)hipFree(h->has_prev);
+    if (h->scratch_i) (void)hipFree(h->scratch_i);
+    if (h->scratch_d) (void)hipFree(h->scratch_d);
+    for (int g = 0; g < kMaxGP; ++g) {
+        if (h->gp_rows[g]) (void)hipFree(h->gp_rows[g]);
+        if (h->gp_vrows[g]) (void)hipFree(h->gp_vrows[g]);
+        if (h->gp_linvT[g]) (void)hipFree(h->gp_linvT[g]);
+    }
+    delete h;
+}
+
+extern "C" {
+
+const char* gpmpc_last_error(void) { return g_err.c_str(); }
+
+int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon) {
+    return (int64_t)sqp_lds_bytes(model_id, horizon);
+}
+
+gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, int32_t device, gpmpc_handle** out) {
+    if (!out) return fail(GPMPC_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    ModelDims md;
+    if (!model_dims(model_id, md)) return fail(GPMPC_ERR_ARG, "unknown model id " + std::to_string(model_id));
+    if (horizon < 1 || horizon > kMaxH) return fail(GPMPC_ERR_ARG, "horizon must be in [1, 63]");
+    if (max_batch < 1) return fail(GPMPC_ERR_ARG, "max_batch must be >= 1");
+    auto* h = new gpmpc_handle();
+    h->device = device;
+    h->model = model_id;
+    h->H = horizon;
+    h->max_batch = max_batch;
+    h->md = md;
+    h->nb = md.nx + md.nu;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(GPMPC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    }
+    const size_t B = max_batch, H = horizon;
+    struct A { void** p; size_t bytes; } allocs[] = {
+        {(void**)&h->x, B * (H + 1) * md.nx * sizeof(double)},
+        {(void**)&h->u, B * H * md.nu * sizeof(double)},
+        {(void**)&h->pi, B * H * md.nx * sizeof(double)},
+        {(void**)&h->lam, B * (H + 1) * 2 * h->nb * sizeof(double)},
+        {(void**)&h->var, B * H * md.ngp * sizeof(double)},
+        {(void**)&h->tight, B * (H + 1) * h->nb * sizeof(double)},
+        {(void**)&h->has_prev, B * sizeof(int32_t)},
+        {(void**)&h->plant_params, kMaxParams * sizeof(double)},
+        {(void**)&h->scratch_i, 2 * B * sizeof(int32_t)},
+        {(void**)&h->scratch_d, 4 * B * sizeof(double)},
+    };
+    for (auto& a : allocs) {
+        e = hipMalloc(a.p, a.bytes);
+        if (e == hipSuccess) e = hipMemset(*a.p, 0, a.bytes);
+        if (e != hipSuccess) {
+            free_handle(h);
+            return fail(GPMPC_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+    }
+    ProblemDev& P = h->P;
+    P.model = model_id;
+    P.nx = md.nx;
+    P.nu = md.nu;
+    P.H = horizon;
+    P.n_gp = md.ngp;
+    P.use_gp = 0;
+    P.cost_scale = 1.0;
+    P.uh = -1e-8;
+    P.tighten = 0;
+    P.max_iter = 25;          // gpmpc.py:262
+    P.tol_stat = P.tol_eq = P.tol_ineq = P.tol_comp = 1e-6;  // acados defaults
+    P.qp_max_iter = 100;
+    P.qp_tol = 1e-10;
+    P.qp_mu0 = 1.0;
+    const size_t lds = sqp_lds_bytes(model_id, horizon);
+    if (lds > 160 * 1024) {
+        free_handle(h);
+        return fail(GPMPC_ERR_ARG, "horizon too long for the LDS budget (" + std::to_string(lds) + " bytes)");
+    }
+    *out = h;
+    return GPMPC_OK;
+}
+
+void gpmpc_destroy(gpmpc_handle* h) { free_handle(h); }
+
+gpmpc_status gpmpc_set_model(gpmpc_handle* h, const double* params, int32_t n_params, double dt, const double* x_lo,
+                             const double* x_hi, const double* u_lo, const double* u_hi, const double* q_diag,
+                             const double* r_diag, const double* u_eq, double uh, int32_t cost_scaling) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (!params || !x_lo || !x_hi || !u_lo || !u_hi || !q_diag || !r_diag || !u_eq)
+        return fail(GPMPC_ERR_ARG, "null array");
+    if (n_params != h->md.nparams)
+        return fail(GPMPC_ERR_ARG, "model expects " + std::to_string(h->md.nparams) + " parameters");
+    if (!(dt > 0.0)) return fail(GPMPC_ERR_ARG, "dt must be > 0");
+    ProblemDev& P = h->P;
+    std::memset(P.params, 0, sizeof(P.params));
+    for (int i = 0; i < n_params; ++i) P.params[i] = params[i];
+    P.dt = dt;
+    for (int i = 0; i < h->md.nx; ++i) {
+        P.x_lo[i] = x_lo[i];
+        P.x_hi[i] = x_hi[i];
+        P.q[i] = q_diag[i];
+        if (!(q_diag[i] >= 0.0)) return fail(GPMPC_ERR_ARG, "q_diag must be >= 0");
+    }
+    for (int a = 0; a < h->md.nu; ++a) {
+        P.u_lo[a] = u_lo[a];
+        P.u_hi[a] = u_hi[a];
+        P.r[a] = r_diag[a];
+        P.u_eq[a] = u_eq[a];
+        if (!(r_diag[a] > 0.0)) return fail(GPMPC_ERR_ARG, "r_diag must be > 0 (GN Hessian)");
+    }
+    P.uh = uh;
+    P.cost_scale = cost_scaling ? dt : 1.0;
+    h->model_set = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_reference(gpmpc_handle* h, const double* traj, int32_t L) {
+    if (!h || !traj || L < 1) return fail(GPMPC_ERR_ARG, "bad reference");
+    (void)hipSetDevice(h->device);
+    const int nx = h->md.nx;
+    std::vector<double> tm((size_t)L * nx);
+    for (int t = 0; t < L; ++t)
+        for (int i = 0; i < nx; ++i) tm[(size_t)t * nx + i] = traj[(size_t)i * L + t];
+    if (h->traj) HIPCHK(hipFree(h->traj));
+    h->traj = nullptr;
+    HIPCHK(hipMalloc(&h->traj, tm.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(h->traj, tm.data(), tm.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->P.traj = h->traj;
+    h->P.traj_len = L;
+    h->ref_set = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_options(gpmpc_handle* h, int32_t max_iter, double tol_stat, double tol_eq, double tol_ineq,
+                               double tol_comp, int32_t qp_max_iter, double qp_tol, double qp_mu0) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (max_iter < 0 || qp_max_iter < 1 || !(qp_mu0 > 0.0)) return fail(GPMPC_ERR_ARG, "bad options");
+    ProblemDev& P = h->P;
+    P.max_iter = max_iter;
+    P.tol_stat = tol_stat;
+    P.tol_eq = tol_eq;
+    P.tol_ineq = tol_ineq;
+    P.tol_comp = tol_comp;
+    P.qp_max_iter = qp_max_iter;
+    P.qp_tol = qp_tol;
+    P.qp_mu0 = qp_mu0;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, const double* X, const double* alpha,
+                          int32_t nv, const double* Xv, const double* Linv, double lengthscale, double outputscale,
+                          double noise) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (gp_id < 0 || gp_id >= h->md.ngp) return fail(GPMPC_ERR_ARG, "gp_id out of range");
+    if (d != h->md.gp_dim[gp_id])
+        return fail(GPMPC_ERR_ARG, "GP " + std::to_string(gp_id) + " expects input dimension " +
+                                       std::to_string(h->md.gp_dim[gp_id]));
+    if (n < 1 || !X || !alpha) return fail(GPMPC_ERR_ARG, "empty GP");
+    if (!(lengthscale > 0.0) || !(outputscale > 0.0) || !(noise >= 0.0)) return fail(GPMPC_ERR_ARG, "bad hyperparameters");
+    if (!Xv) { Xv = X; nv = n; }
+    if (nv < 1) return fail(GPMPC_ERR_ARG, "empty variance GP");
+    (void)hipSetDevice(h->device);
+    auto pack = [&](const double* Xs, const double* w, int m, std::vector<double>& out) {
+        const int mp = (m + 15) / 16 * 16;
+        out.assign((size_t)mp * 4, 0.0);
+        for (int i = 0; i < m; ++i) {
+            for (int k = 0; k < d; ++k) out[(size_t)i * 4 + k] = Xs[(size_t)i * d + k];
+            out[(size_t)i * 4 + 3] = w ? w[i] : 0.0;
+        }
+    };
+    std::vector<double> rows, vrows;
+    pack(X, alpha, n, rows);
+    const bool exact = (Xv == X);
+    if (!exact) pack(Xv, nullptr, nv, vrows);
+    const int npad = (nv + 15) / 16 * 16;
+    for (double** p : {&h->gp_rows[gp_id], &h->gp_vrows[gp_id], &h->gp_linvT[gp_id]}) {
+        if (*p) HIPCHK(hipFree(*p));
+        *p = nullptr;
+    }
+    HIPCHK(hipMalloc(&h->gp_rows[gp_id], rows.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(h->gp_rows[gp_id], rows.data(), rows.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (!exact) {
+        HIPCHK(hipMalloc(&h->gp_vrows[gp_id], vrows.size() * sizeof(double)));
+        HIPCHK(hipMemcpy(h->gp_vrows[gp_id], vrows.data(), vrows.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (Linv) {
+        std::vector<double> lt((size_t)npad * npad, 0.0);
+        for (int i = 0; i < nv; ++i)
+            for (int j = 0; j <= i; ++j) lt[(size_t)j * npad + i] = Linv[(size_t)i * nv + j];  // (L^-1)^T
+        HIPCHK(hipMalloc(&h->gp_linvT[gp_id], lt.size() * sizeof(double)));
+        HIPCHK(hipMemcpy(h->gp_linvT[gp_id], lt.data(), lt.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    GPDev& g = h->P.gp[gp_id];
+    g.rows = h->gp_rows[gp_id];
+    g.vrows = exact ? h->gp_rows[gp_id] : h->gp_vrows[gp_id];
+    g.linvT = h->gp_linvT[gp_id];
+    g.n = n;
+    g.nv = nv;
+    g.d = d;
+    g.inv_ell2 = 1.0 / (lengthscale * lengthscale);
+    g.sf2 = outputscale;
+    g.sn2 = noise;
+    h->gp_npad[gp_id] = npad;
+    h->gp_set[gp_id] = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (enabled)
+        for (int g = 0; g < h->md.ngp; ++g)
+            if (!h->gp_set[g]) return fail(GPMPC_ERR_STATE, "GP " + std::to_string(g) + " not set");
+    h->P.use_gp = enabled ? 1 : 0;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_tightening(gpmpc_handle* h, int32_t enabled, double inverse_cdf, const double* Ad,
+                                  const double* Bd, const double* K) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    ProblemDev& P = h->P;
+    P.tighten = enabled ? 1 : 0;
+    if (!enabled) return GPMPC_OK;
+    if (!Ad || !Bd || !K) return fail(GPMPC_ERR_ARG, "null tightening matrices");
+    const int nx = h->md.nx, nu = h->md.nu;
+    P.icdf = inverse_cdf;
+    for (int i = 0; i < nx; ++i)
+        for (int j = 0; j < nx; ++j) {
+            double acc = Ad[i * nx + j];
+            for (int a = 0; a < nu; ++a) acc += Bd[i * nu + a] * K[a * nx + j];
+            P.Acl[i * nx + j] = acc;
+        }
+    for (int a = 0; a < nu * nx; ++a) P.K[a] = K[a];
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, void* stream) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t B = batch, H = h->H;
+    HIPCHK(hipMemsetAsync(h->has_prev, 0, B * sizeof(int32_t), s));
+    if (reset_iterate) {
+        HIPCHK(hipMemsetAsync(h->x, 0, B * (H + 1) * h->md.nx * sizeof(double), s));
+        HIPCHK(hipMemsetAsync(h->u, 0, B * H * h->md.nu * sizeof(double), s));
+        HIPCHK(hipMemsetAsync(h->pi, 0, B * H * h->md.nx * sizeof(double), s));
+        HIPCHK(hipMemsetAsync(h->lam, 0, B * (H + 1) * 2 * h->nb * sizeof(double), s));
+    }
+    if (batch == h->max_batch) h->any_prev = false;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_dev, const double* u_dev, void* stream) {
+    if (!h || !x_dev || !u_dev) return fail(GPMPC_ERR_ARG, "null argument");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t B = batch, H = h->H;
+    HIPCHK(hipMemcpyAsync(h->x, x_dev, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(h->u, u_dev, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemsetAsync(h->pi, 0, B * H * h->md.nx * sizeof(double), s));
+    HIPCHK(hipMemsetAsync(h->lam, 0, B * (H + 1) * 2 * h->nb * sizeof(double), s));
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const int32_t* tstep, double* u0,
+                         int32_t* status, int32_t* sqp_iter, int32_t* qp_iter, double* res, void* stream) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (!h->model_set) return fail(GPMPC_ERR_STATE, "gpmpc_set_model not called");
+    if (!h->ref_set) return fail(GPMPC_ERR_STATE, "gpmpc_set_reference not called");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    if (!x0 || !tstep || !u0 || !status) return fail(GPMPC_ERR_ARG, "null output/input");
+    if (h->P.tighten && h->P.use_gp)
+        for (int g = 0; g < h->md.ngp; ++g)
+            if (!h->gp_linvT[g]) return fail(GPMPC_ERR_STATE, "tightening needs Linv for every GP");
+    (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    ProblemDev P = h->P;
+    P.tighten = (h->P.tighten && h->P.use_gp) ? 1 : 0;
+    // 1. GP variances at the previous solution (the MFMA contraction), only when needed
+    if (P.tighten && h->any_prev) {
+        for (int g = 0; g < h->md.ngp; ++g) {
+            PostArgs a{};
+            a.sx = h->x;
+            a.su = h->u;
+            a.H = h->H;
+            a.nx = h->md.nx;
+            a.nu = h->md.nu;
+            a.ngp = h->md.ngp;
+            a.gp_index = g;
+            for (int k = 0; k < 3; ++k) a.src[k] = h->md.var_src[g][k];
+            a.P = batch * h->H;
+            a.d = h->md.gp_dim[g];
+            a.with_noise = 1;   // gp.likelihood(gp(z)) (gpmpc.py:444)
+            a.mean = nullptr;
+            a.var = h->var;
+            a.var_stride = h->md.ngp;
+            a.var_off = g;
+            HIPCHK(launch_gp_post(P.gp[g], h->gp_npad[g], a, true, s));
+        }
+    }
+    // 2. the SQP step
+    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight};
+    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res};
+    // optional outputs go to handle-owned scratch when NULL
+    if (!io.sqp_iter) io.sqp_iter = h->scratch_i;
+    if (!io.qp_iter) io.qp_iter = h->scratch_i + h->max_batch;
+    if (!io.res) io.res = h->scratch_d;
+    HIPCHK(launch_sqp(P, S, io, batch, s));
+    h->any_prev = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, double* u_dev, double* tight_dev,
+                                void* stream) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    const size_t B = batch, H = h->H;
+    if (x_dev) HIPCHK(hipMemcpyAsync(x_dev, h->x, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (u_dev) HIPCHK(hipMemcpyAsync(u_dev, h->u, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
+    if (tight_dev)
+        HIPCHK(hipMemcpyAsync(tight_dev, h->tight, B * (H + 1) * h->nb * sizeof(double), hipMemcpyDeviceToDevice, s));
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_gp_predict(gpmpc_handle* h, int32_t gp_id, const double* Z, int32_t P, double* mean, double* var,
+                              int32_t with_noise, void* stream) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (gp_id < 0 || gp_id >= h->md.ngp || !h->gp_set[gp_id]) return fail(GPMPC_ERR_STATE, "GP not set");
+    if (P < 0 || (P > 0 && !Z)) return fail(GPMPC_ERR_ARG, "bad points");
+    if (var && !h->gp_linvT[gp_id]) return fail(GPMPC_ERR_STATE, "variance needs Linv");
+    if (P == 0) return GPMPC_OK;
+    (void)hipSetDevice(h->device);
+    const GPDev& g = h->P.gp[gp_id];
+    PostArgs a{};
+    a.Z = Z;
+    a.ldz = h->md.gp_dim[gp_id];
+    a.P = P;
+    a.d = h->md.gp_dim[gp_id];
+    a.with_noise = with_noise;
+    a.var_stride = 1;
+    a.var_off = 0;
+    if (mean) {  // mean over the mean set (exact: training set; FITC: inducing set)
+        GPDev gm = g;
+        gm.vrows = g.rows;
+        gm.nv = g.n;
+        gm.linvT = nullptr;
+        a.mean = mean;
+        a.var = nullptr;
+        HIPCHK(launch_gp_post(gm, (g.n + 15) / 16 * 16, a, false, (hipStream_t)stream));
+    }
+    if (var) {
+        a.mean = nullptr;
+        a.var = var;
+        HIPCHK(launch_gp_post(g, h->gp_npad[gp_id], a, false, (hipStream_t)stream));
+    }
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double* rows, const double* linvT,
+                                double lengthscale, double outputscale, double noise, const double* Z, int32_t P,
+                                double* mean, double* var, int32_t with_noise, void* stream) {
+    if (n < 1 || d < 1 || d > kMaxGPDim || npad < n || npad % 16 != 0 || !rows)
+        return fail(GPMPC_ERR_ARG, "bad GP layout (need 1 <= d <= 3, npad = 16-multiple >= n)");
+    if (P < 0 || (P > 0 && !Z)) return fail(GPMPC_ERR_ARG, "bad points");
+    if (var && !linvT) return fail(GPMPC_ERR_ARG, "variance needs linvT");
+    if (!(lengthscale > 0.0) || !(outputscale > 0.0) || !(noise >= 0.0)) return fail(GPMPC_ERR_ARG, "bad hyperparameters");
+    if (P == 0) return GPMPC_OK;
+    GPDev g{rows, rows, linvT, n, n, d, 1.0 / (lengthscale * lengthscale), outputscale, noise};
+    PostArgs a{};
+    a.Z = Z;
+    a.ldz = d;
+    a.P = P;
+    a.d = d;
+    a.with_noise = with_noise;
+    a.mean = mean;
+    a.var = var;
+    a.var_stride = 1;
+    a.var_off = 0;
+    HIPCHK(launch_gp_post(g, npad, a, false, (hipStream_t)stream));
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* params, const double* x, const double* u,
+                              double* x_next, int32_t* tstep, void* stream) {
+    if (!h || !params || !x || !u || !x_next) return fail(GPMPC_ERR_ARG, "null argument");
+    if (batch < 1) return fail(GPMPC_ERR_ARG, "batch out of range");
+    (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    bool same = h->plant_params_valid;
+    for (int i = 0; i < h->md.nparams; ++i) same = same && (h->plant_params_host[i] == params[i]);
+    if (!same) {  // synchronous upload of a 16-double table, only when the parameters change
+        for (int i = 0; i < kMaxParams; ++i) h->plant_params_host[i] = i < h->md.nparams ? params[i] : 0.0;
+        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hipMemcpy(h->plant_params, h->plant_params_host, sizeof(h->plant_params_host), hipMemcpyHostToDevice));
+        h->plant_params_valid = true;
+    }
+    HIPCHK(launch_plant(h->model, h->plant_params, h->P.dt, x, u, x_next, tstep, batch, s));
+    return GPMPC_OK;
+}
+
+}  // extern "C"

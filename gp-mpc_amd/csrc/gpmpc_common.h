@@ -1,0 +1,105 @@
+// Shared host/device definitions for the MI355X GP-MPC solve path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gpmpc {
+
+constexpr int kMaxGP = 4;       // GPs per model (quad3d: 3)
+constexpr int kMaxGPDim = 3;    // inputs per GP (packed rows are 4 doubles: x0,x1,x2,alpha)
+constexpr int kMaxNX = 12;
+constexpr int kMaxNU = 4;
+constexpr int kMaxH = 63;       // one lane per stage 0..H (64-lane wavefront)
+constexpr int kMaxParams = 16;
+
+enum ModelId : int32_t { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };
+
+// acados status codes (acados_c/ocp_nlp_interface.h) -- gpmpc/gpmpc.py:365
+enum SolveStatus : int32_t { kSuccess = 0, kNaN = 1, kMaxIter = 2, kMinStep = 3, kQPFailure = 4 };
+
+// One GP replica in device memory.
+struct GPDev {
+    const double* rows;   // [n][4]: mean inputs (d <= 3, zero padded) + weight alpha = K^-1 y (gpmpc/gp.py:84-85)
+                          //         (FITC: inducing inputs + posterior weights, gpmpc/gpmpc.py:377-400)
+    const double* vrows;  // [nv][4]: training inputs of the variance GP (== rows for an exact GP)
+    const double* linvT;  // [npad][npad] row-major (L^-1)^T, L = chol(K); NULL -> no variance
+    int32_t n;
+    int32_t nv;
+    int32_t d;
+    double inv_ell2;      // 1 / lengthscale^2 (isotropic RBF, gpmpc/gp.py:34)
+    double sf2;           // outputscale
+    double sn2;           // likelihood noise (gpmpc/gp.py:31)
+};
+
+// Everything the per-step kernels need, passed by value.
+struct ProblemDev {
+    int32_t model;
+    int32_t nx, nu, H;
+    int32_t n_gp;
+    int32_t use_gp;           // 0: nominal MPC (gpmpc/mpc.py)
+    double dt;
+    double cost_scale;        // acados cost_scaling for stages 0..H-1 (time step), 1 for terminal
+    double uh;                // h <= uh: -1e-8 GPMPC (gpmpc.py:309-314), +1e-8 MPC (mpc.py:242-247)
+    double params[kMaxParams];
+    double x_lo[kMaxNX], x_hi[kMaxNX], u_lo[kMaxNU], u_hi[kMaxNU];
+    double q[kMaxNX], r[kMaxNU], u_eq[kMaxNU];
+    // reference trajectory (nx, L) column-major by time: traj[t * nx + i]   (gpmpc.py:509-514)
+    const double* traj;
+    int32_t traj_len;
+    // tightening (gpmpc.py:425-498)
+    int32_t tighten;
+    double icdf;
+    double Acl[kMaxNX * kMaxNX];   // A_d + B_d K_lqr (the four-term update of gpmpc.py:489-495)
+    double K[kMaxNU * kMaxNX];     // K_lqr
+    // SQP / QP options (gpmpc.py:257-263; acados default tolerances)
+    int32_t max_iter, qp_max_iter;
+    double tol_stat, tol_eq, tol_ineq, tol_comp, qp_tol, qp_mu0;
+    GPDev gp[kMaxGP];
+};
+
+// Per-instance state owned by the handle (acados keeps the same in its memory).
+struct StateDev {
+    double* x;        // [B][H+1][nx] iterate / previous solution (x_prev)
+    double* u;        // [B][H][nu]
+    double* pi;       // [B][H][nx]  dynamics multipliers
+    double* lam;      // [B][H+1][2*nb] bound multipliers (lower | upper), nb = nx+nu
+    int32_t* has_prev;   // [B] previous solution valid -> tighten (gpmpc.py:432-433)
+    const double* var;   // [B][H][n_gp] GP variances at the previous solution (incl. noise)
+    double* tight;       // [B][H+1][2*nb] tightening values (state lo|hi, input lo|hi), optional
+};
+
+struct StepIO {
+    const double* x0;        // [B][nx]
+    const int32_t* tstep;    // [B] reference index
+    double* u0;              // [B][nu] out
+    int32_t* status;         // [B] out
+    int32_t* sqp_iter;       // [B] out
+    int32_t* qp_iter;        // [B] out, total IPM iterations
+    double* res;             // [B][4] out, final NLP residuals (stat, eq, ineq, comp)
+};
+
+// Arguments of the GP posterior kernel (gp_kernels.hip).
+struct PostArgs {
+    // points: either dense Z[P][ldz] (first d columns), or gathered from the solver state
+    const double* Z;
+    int32_t ldz;
+    const double* sx;     // state x [B][H+1][nx]
+    const double* su;     // state u [B][H][nu]
+    int32_t H, nx, nu, ngp, gp_index;
+    int32_t src[3];       // var input map into z = [x; u] (gpmpc.py:437-444)
+    int32_t P;            // number of points
+    int32_t d;
+    int32_t with_noise;
+    double* mean;         // [P] or null
+    double* var;          // var[p * var_stride + var_off] or null
+    int32_t var_stride, var_off;
+};
+
+// Launchers (sqp_kernel.hip, gp_kernels.hip).
+hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream);
+size_t sqp_lds_bytes(int model, int H);
+hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream);
+hipError_t launch_plant(int model, const double* params, double dt, const double* x, const double* u, double* xn,
+                        int32_t* tstep, int B, hipStream_t stream);
+
+}  // namespace gpmpc

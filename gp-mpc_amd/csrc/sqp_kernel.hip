@@ -1,0 +1,934 @@
+// Batched GP-MPC control step on CDNA4 (gfx950): one 64-lane wavefront per MPC instance.
+//
+// One launch = one call of GPMPC.select_action for B instances (gpmpc/gpmpc.py:334-368):
+//   1. constraint tightening from the previous solution      (gpmpc/gpmpc.py:425-498)
+//      -- the GP variances come from gp_var_kernel (gp_kernels.hip)
+//   2. acados-style SQP, Gauss-Newton Hessian, full steps,   (gpmpc/gpmpc.py:257-264)
+//      status codes 0/1/2/4 (gpmpc/gpmpc.py:365)
+//      a. linearisation: RK4 of prior + GP residual, exact tangent map (gpmpc/gpmpc.py:166-221)
+//         -- GP mean + gradient sums over the training set, split over lane chunks
+//      b. NLP residuals (stat / eq / ineq / comp) with the previous multipliers
+//      c. box-constrained LQ sub-problem: Mehrotra primal-dual IPM whose Newton systems
+//         are solved by a Riccati recursion over the horizon (the HPIPM structure)
+//   3. u0, the new iterate (= x_prev/u_prev for the next step) and the multipliers.
+//
+// Lane layout: lane k (0..H) owns stage k: w_k = [x_k; u_k] (x_0 fixed to obs, u_H absent),
+// its bounds, IPM slacks/multipliers and the dynamics multiplier pi_k.  The Riccati
+// recursion is sequential over stages and parallel over matrix entries (lanes).
+#include "gpmpc_common.h"
+#include "models.h"
+
+namespace gpmpc {
+
+#define WSYNC() __syncthreads()  // block == one wavefront: orders LDS traffic of the wave
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// In-register inverse of a small SPD matrix (Gauss-Jordan, no pivoting needed for SPD).
+template <int N>
+__device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) inv[i][j] = (i == j) ? 1.0 : 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < N; ++c) {
+        const double piv = a[c][c];
+        ok = ok && (piv > 0.0);
+        const double r = 1.0 / piv;
+#pragma unroll
+        for (int j = 0; j < N; ++j) { a[c][j] *= r; inv[c][j] *= r; }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            if (i == c) continue;
+            const double f = a[i][c];
+#pragma unroll
+            for (int j = 0; j < N; ++j) { a[i][j] -= f * a[c][j]; inv[i][j] -= f * inv[c][j]; }
+        }
+    }
+    return ok;
+}
+
+// Partial GP sums over training rows [i0, i1): m = sum alpha_i e_i, g_d = sum alpha_i e_i (x_id - z_d),
+// e_i = exp(-0.5 |z - x_i|^2 / ell^2)  (gpmpc/gp.py:12-14, 84-85; alpha = K^-1 y).
+template <int D>
+__device__ __forceinline__ void gp_partial(const GPDev& g, const double* z, int i0, int i1, double& m, double (&gacc)[3]) {
+    const double c = -0.5 * g.inv_ell2;
+    double m0 = 0.0, m1 = 0.0;
+    double a0[3] = {0, 0, 0}, a1[3] = {0, 0, 0};
+    const double4* rows = reinterpret_cast<const double4*>(g.rows);
+    int i = i0;
+    for (; i + 1 < i1; i += 2) {
+        const double4 ra = rows[i], rb = rows[i + 1];
+        const double xa[3] = {ra.x, ra.y, ra.z}, xb[3] = {rb.x, rb.y, rb.z};
+        double qa = 0.0, qb = 0.0, da[3], db[3];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            da[d] = xa[d] - z[d];
+            db[d] = xb[d] - z[d];
+            qa = fma(da[d], da[d], qa);
+            qb = fma(db[d], db[d], qb);
+        }
+        const double wa = ra.w * exp(c * qa), wb = rb.w * exp(c * qb);
+        m0 += wa;
+        m1 += wb;
+#pragma unroll
+        for (int d = 0; d < D; ++d) { a0[d] = fma(wa, da[d], a0[d]); a1[d] = fma(wb, db[d], a1[d]); }
+    }
+    if (i < i1) {
+        const double4 ra = rows[i];
+        const double xa[3] = {ra.x, ra.y, ra.z};
+        double qa = 0.0, da[3];
+#pragma unroll
+        for (int d = 0; d < D; ++d) { da[d] = xa[d] - z[d]; qa = fma(da[d], da[d], qa); }
+        const double wa = ra.w * exp(c * qa);
+        m0 += wa;
+#pragma unroll
+        for (int d = 0; d < D; ++d) a0[d] = fma(wa, da[d], a0[d]);
+    }
+    m = m0 + m1;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) gacc[d] = (d < D) ? a0[d] + a1[d] : 0.0;
+}
+
+template <int ID>
+struct SqpKernel {
+    using M = Model<ID>;
+    static constexpr int NX = M::NX, NU = M::NU, NB = M::NB, NGP = M::NGP, NUNC = M::NUNC;
+    static constexpr int CB = 4;                       // tangent column block
+    static constexpr int NCB = (NB + CB - 1) / CB;
+
+    // LDS carve (doubles), sized by H at launch.
+    struct Lds {
+        double *G, *P, *p, *K, *kff, *Rui, *hq, *gq, *cc, *dxv, *W, *Ms, *vs, *cd, *Sig;
+    };
+    __host__ __device__ static size_t lds_doubles(int H) {
+        return (size_t)H * NX * NB          // G_k = [A_k B_k]
+               + (size_t)(H + 1) * NX * NX  // P_k
+               + (size_t)(H + 1) * NX       // p_k
+               + (size_t)H * NU * NX        // K_k
+               + (size_t)H * NU             // kff_k
+               + (size_t)H * NU * NU        // Ru_k^-1
+               + (size_t)(H + 1) * NB * 2   // hq, gq
+               + (size_t)H * NX             // cc
+               + (size_t)(H + 1) * NX       // dx
+               + (size_t)NX * NB + NB * NB + 2 * NB + NX  // W, M, vectors
+               + (size_t)H * NUNC           // cov_d diag per stage
+               + (size_t)2 * NX * NX + NU * NX;  // Sigma, T scratch
+    }
+    __device__ static Lds carve(double* s, int H) {
+        Lds L;
+        L.G = s;   s += (size_t)H * NX * NB;
+        L.P = s;   s += (size_t)(H + 1) * NX * NX;
+        L.p = s;   s += (size_t)(H + 1) * NX;
+        L.K = s;   s += (size_t)H * NU * NX;
+        L.kff = s; s += (size_t)H * NU;
+        L.Rui = s; s += (size_t)H * NU * NU;
+        L.hq = s;  s += (size_t)(H + 1) * NB;
+        L.gq = s;  s += (size_t)(H + 1) * NB;
+        L.cc = s;  s += (size_t)H * NX;
+        L.dxv = s; s += (size_t)(H + 1) * NX;
+        L.W = s;   s += (size_t)NX * NB;
+        L.Ms = s;  s += (size_t)NB * NB;
+        L.vs = s;  s += (size_t)2 * NB + NX;
+        L.cd = s;  s += (size_t)H * NUNC;
+        L.Sig = s;
+        return L;
+    }
+
+    // ------------------------------------------------------------------ GP sum, chunked over lanes
+    // All lanes of stage s (lanes s + c*H, c < C) hold the same point z; each sums its chunk
+    // of the training set and the partial sums are combined across the C lanes.
+    template <int G>
+    __device__ static void gp_eval(const ProblemDev& P, const double* z, int stage, int chunk, int C, int H,
+                                   double& m, double (&gg)[3]) {
+        constexpr int D = M::gp_dim[G];
+        const GPDev& g = P.gp[G];
+        const int per = (g.n + C - 1) / C;
+        const int i0 = min(g.n, chunk * per), i1 = min(g.n, i0 + per);
+        double part, gacc[3];
+        gp_partial<D>(g, z, i0, i1, part, gacc);
+        double tm = 0.0, tg[3] = {0, 0, 0};
+        for (int c = 0; c < C; ++c) {
+            const int src = stage + c * H;
+            tm += __shfl(part, src);
+#pragma unroll
+            for (int d = 0; d < D; ++d) tg[d] += __shfl(gacc[d], src);
+        }
+        m = g.sf2 * tm;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) gg[d] = (d < D) ? g.sf2 * g.inv_ell2 * tg[d] : 0.0;
+    }
+
+    template <int G>
+    __device__ static void gp_input(const double* x, const double* u, double* z) {
+#pragma unroll
+        for (int d = 0; d < M::gp_dim[G]; ++d) {
+            const int s = M::gp_src[G][d];
+            z[d] = s < NX ? x[s] : u[s - NX];
+        }
+    }
+
+    template <int G>
+    __device__ static void eval_gp_if(const ProblemDev& P, bool state_pass, const double* x, const double* u, int stage,
+                                      int chunk, int C, int H, double* gm, double (*gg)[3]) {
+        if (M::gp_state_dep[G] == state_pass) {
+            double z[3];
+            gp_input<G>(x, u, z);
+            gp_eval<G>(P, z, stage, chunk, C, H, gm[G], gg[G]);
+        }
+    }
+
+    __device__ static void eval_gps(const ProblemDev& P, bool state_pass, const double* x, const double* u, int stage,
+                                    int chunk, int C, int H, double* gm, double (*gg)[3]) {
+        if (!P.use_gp) {
+            if (!state_pass)
+                for (int g = 0; g < NGP; ++g) { gm[g] = 0.0; gg[g][0] = gg[g][1] = gg[g][2] = 0.0; }
+            return;
+        }
+        eval_gp_if<0>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
+        if constexpr (NGP > 1) eval_gp_if<1>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
+        if constexpr (NGP > 2) eval_gp_if<2>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
+    }
+
+    // ------------------------------------------------------------------ linearisation
+    // Every lane computes RK4 for stage s = lane % H (its chunk of the GP sums); chunk-c lanes
+    // then build tangent column blocks jb with jb % C == c.  Lane s (chunk 0) returns F_s.
+    __device__ static void linearize(const ProblemDev& P, const Lds& L, int H, int lane, const double (&w)[NB],
+                                     double (&F)[NX]) {
+        const int C = max(1, 64 / H);
+        const int stage = lane % H;
+        const int chunk = lane < C * H ? lane / H : C;  // chunk C: empty training range
+        double x[NX], u[NU];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x[i] = __shfl(w[i], stage);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) u[a] = __shfl(w[NX + a], stage);
+
+        const double h = P.dt;
+        double xs[4][NX], gm[4][NGP], gg[4][NGP][3];
+        double gm0[NGP], gg0[NGP][3];
+        eval_gps(P, false, x, u, stage, chunk, C, H, gm0, gg0);  // GPs of u only: once per stage
+        double kprev[NX], acc[NX];
+        const double cs[4] = {0.0, 0.5, 0.5, 1.0}, ws[4] = {1.0, 2.0, 2.0, 1.0};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xs[s][i] = (s == 0) ? x[i] : fma(cs[s] * h, kprev[i], x[i]);
+#pragma unroll
+            for (int g = 0; g < NGP; ++g) {
+                gm[s][g] = gm0[g];
+                gg[s][g][0] = gg0[g][0]; gg[s][g][1] = gg0[g][1]; gg[s][g][2] = gg0[g][2];
+            }
+            eval_gps(P, true, xs[s], u, stage, chunk, C, H, gm[s], gg[s]);
+            M::f(P.params, xs[s], u, gm[s], kprev);
+#pragma unroll
+            for (int i = 0; i < NX; ++i) acc[i] = (s == 0) ? kprev[i] : fma(ws[s], kprev[i], acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) F[i] = fma(h / 6.0, acc[i], x[i]);
+
+        // tangent map of the RK4 step, column block by column block
+        for (int jb = 0; jb < NCB; ++jb) {
+            if (jb % C != (chunk < C ? chunk : -1)) continue;
+            const int j0 = jb * CB;
+            double V[NX][CB], dk[NX][CB], dF[NX][CB];
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+#pragma unroll
+                for (int j = 0; j < CB; ++j) { V[i][j] = (i == j0 + j) ? 1.0 : 0.0; dF[i][j] = V[i][j]; }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                M::template tangent<CB>(P.params, xs[s], u, gm[s], gg[s], V, j0, dk);
+                const double cn = (s < 3) ? cs[s + 1] * h : 0.0;
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+#pragma unroll
+                    for (int j = 0; j < CB; ++j) {
+                        dF[i][j] = fma(h / 6.0 * ws[s], dk[i][j], dF[i][j]);
+                        V[i][j] = fma(cn, dk[i][j], (i == j0 + j) ? 1.0 : 0.0);
+                    }
+            }
+            if (chunk < C) {
+                double* Gs = L.G + (size_t)stage * NX * NB;
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+#pragma unroll
+                    for (int j = 0; j < CB; ++j)
+                        if (j0 + j < NB) Gs[i * NB + j0 + j] = dF[i][j];
+            }
+        }
+    }
+
+
+    // ------------------------------------------------------------------ Riccati recursion
+    // Newton system of the IPM: min sum_k 1/2 w_k' diag(hq_k) w_k + gq_k' w_k
+    //   s.t. dx_{k+1} = A_k dx_k + B_k du_k + cc_k, dx_0 = 0.
+    // Backward sweep (factorisation + vector); stores K_k, kff_k, Ru_k^-1, P_k, p_k.
+    __device__ static bool riccati_factor(const Lds& L, int H, int lane) {
+        // P_H = diag(hq_H[x]), p_H = gq_H[x]
+        double* PH = L.P + (size_t)H * NX * NX;
+        for (int e = lane; e < NX * NX; e += 64) PH[e] = (e / NX == e % NX) ? L.hq[H * NB + e / NX] : 0.0;
+        if (lane < NX) L.p[H * NX + lane] = L.gq[H * NB + lane];
+        WSYNC();
+        bool ok = true;
+        for (int k = H - 1; k >= 0; --k) {
+            const double* Pn = L.P + (size_t)(k + 1) * NX * NX;
+            const double* pn = L.p + (size_t)(k + 1) * NX;
+            const double* G = L.G + (size_t)k * NX * NB;
+            const double* c = L.cc + (size_t)k * NX;
+            double* pv = L.vs;            // NX
+            double* gv = L.vs + NX;       // NB
+            // phase 1: W = P_{k+1} G_k, pv = P_{k+1} c_k + p_{k+1}
+            for (int e = lane; e < NX * NB + NX; e += 64) {
+                if (e < NX * NB) {
+                    const int l = e / NB, j = e % NB;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) acc = fma(Pn[l * NX + m], G[m * NB + j], acc);
+                    L.W[e] = acc;
+                } else {
+                    const int i = e - NX * NB;
+                    double acc = pn[i];
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) acc = fma(Pn[i * NX + m], c[m], acc);
+                    pv[i] = acc;
+                }
+            }
+            WSYNC();
+            // phase 2: M = diag(hq_k) + G' W, gv = gq_k + G' pv
+            for (int e = lane; e < NB * NB + NB; e += 64) {
+                if (e < NB * NB) {
+                    const int i = e / NB, j = e % NB;
+                    double acc = (i == j) ? L.hq[k * NB + i] : 0.0;
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + i], L.W[l * NB + j], acc);
+                    L.Ms[e] = acc;
+                } else {
+                    const int j = e - NB * NB;
+                    double acc = L.gq[k * NB + j];
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + j], pv[l], acc);
+                    gv[j] = acc;
+                }
+            }
+            WSYNC();
+            // phase 3: Schur complement onto the state block
+            double Ru[NU][NU], Ri[NU][NU];
+#pragma unroll
+            for (int a = 0; a < NU; ++a)
+#pragma unroll
+                for (int b2 = 0; b2 < NU; ++b2) Ru[a][b2] = L.Ms[(NX + a) * NB + NX + b2];
+            ok = spd_inverse<NU>(Ru, Ri) && ok;
+            const int nP = (k >= 1) ? NX * NX : 0;
+            for (int e = lane; e < nP + NX + NU * NX + NU + NU * NU; e += 64) {
+                if (e < nP) {
+                    const int i = e / NX, j = e % NX;
+                    double acc = L.Ms[i * NB + j];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        double t = 0.0;
+#pragma unroll
+                        for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], L.Ms[(NX + b2) * NB + j], t);
+                        acc = fma(-L.Ms[(NX + a) * NB + i], t, acc);
+                    }
+                    L.P[(size_t)k * NX * NX + e] = acc;
+                } else if (e < nP + NX) {
+                    const int i = e - nP;
+                    double acc = gv[i];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        double t = 0.0;
+#pragma unroll
+                        for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], gv[NX + b2], t);
+                        acc = fma(-L.Ms[(NX + a) * NB + i], t, acc);
+                    }
+                    L.p[(size_t)k * NX + i] = acc;
+                } else if (e < nP + NX + NU * NX) {
+                    const int q = e - nP - NX, a = q / NX, i = q % NX;
+                    double t = 0.0;
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], L.Ms[(NX + b2) * NB + i], t);
+                    L.K[(size_t)k * NU * NX + q] = -t;
+                } else if (e < nP + NX + NU * NX + NU) {
+                    const int a = e - nP - NX - NU * NX;
+                    double t = 0.0;
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], gv[NX + b2], t);
+                    L.kff[k * NU + a] = -t;
+                } else {
+                    const int q = e - nP - NX - NU * NX - NU;
+                    L.Rui[(size_t)k * NU * NU + q] = Ri[q / NU][q % NU];
+                }
+            }
+            WSYNC();
+        }
+        return ok;
+    }
+
+    // Vector-only backward sweep with the stored factorisation (Mehrotra corrector).
+    __device__ static void riccati_vector(const Lds& L, int H, int lane) {
+        if (lane < NX) L.p[H * NX + lane] = L.gq[H * NB + lane];
+        WSYNC();
+        for (int k = H - 1; k >= 0; --k) {
+            const double* Pn = L.P + (size_t)(k + 1) * NX * NX;
+            const double* pn = L.p + (size_t)(k + 1) * NX;
+            const double* G = L.G + (size_t)k * NX * NB;
+            const double* c = L.cc + (size_t)k * NX;
+            double* pv = L.vs;
+            if (lane < NX) {
+                double acc = pn[lane];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) acc = fma(Pn[lane * NX + m], c[m], acc);
+                pv[lane] = acc;
+            }
+            WSYNC();
+            // gv_j = gq_kj + sum_l G_lj pv_l ; p_k = gv_x + K' gv_u ; kff = -Ru^-1 gv_u
+            if (lane < NX + NU) {
+                double gu[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double acc = L.gq[k * NB + NX + a];
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + NX + a], pv[l], acc);
+                    gu[a] = acc;
+                }
+                if (lane < NX) {
+                    if (k >= 1) {
+                        const int i = lane;
+                        double acc = L.gq[k * NB + i];
+#pragma unroll
+                        for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + i], pv[l], acc);
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) acc = fma(L.K[(size_t)k * NU * NX + a * NX + i], gu[a], acc);
+                        L.p[(size_t)k * NX + i] = acc;
+                    }
+                } else {
+                    const int a = lane - NX;
+                    double t = 0.0;
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) t = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], gu[b2], t);
+                    L.kff[k * NU + a] = -t;
+                }
+            }
+            WSYNC();
+        }
+    }
+
+    // Forward sweep: dx_0 = 0, du_k = K_k dx_k + kff_k, dx_{k+1} = A dx_k + B du_k + cc_k.
+    __device__ static void riccati_forward(const Lds& L, int H, int lane) {
+        if (lane < NX) L.dxv[lane] = 0.0;
+        WSYNC();
+        for (int k = 0; k < H; ++k) {
+            if (lane < NX) {
+                const double* dx = L.dxv + (size_t)k * NX;
+                const double* G = L.G + (size_t)k * NX * NB;
+                double xk[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) xk[j] = dx[j];
+                double acc = L.cc[k * NX + lane];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) acc = fma(G[lane * NB + j], xk[j], acc);
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double du = L.kff[k * NU + a];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) du = fma(L.K[(size_t)k * NU * NX + a * NX + j], xk[j], du);
+                    acc = fma(G[lane * NB + NX + a], du, acc);
+                }
+                L.dxv[(size_t)(k + 1) * NX + lane] = acc;
+            }
+            WSYNC();
+        }
+    }
+
+    // Per-lane step from the Riccati solution: dd (stage k variables) and dpi_k.
+    __device__ static void recover_step(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        const bool on = lane <= H;
+        double dx[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dx[i] = (on && lane >= 1) ? L.dxv[(size_t)lane * NX + i] : 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dd[i] = dx[i];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double du = 0.0;
+            if (lane < H) {
+                du = L.kff[lane * NU + a];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) du = fma(L.K[(size_t)lane * NU * NX + a * NX + j], dx[j], du);
+            }
+            dd[NX + a] = du;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = 0.0;
+            if (lane < H) {
+                acc = L.p[(size_t)(lane + 1) * NX + i];
+#pragma unroll
+                for (int j = 0; j < NX; ++j)
+                    acc = fma(L.P[(size_t)(lane + 1) * NX * NX + i * NX + j], L.dxv[(size_t)(lane + 1) * NX + j], acc);
+            }
+            dpi[i] = -acc;
+        }
+    }
+
+    // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
+    __device__ static void ctpi(const Lds& L, int H, int lane, const double (&pi)[NX], double (&out)[NB]) {
+        double pim1[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pim1[i] = __shfl(pi[i], lane > 0 ? lane - 1 : 0);
+        const double* G = L.G + (size_t)min(lane, H - 1) * NX * NB;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            double acc = 0.0;
+            if (lane < H) {
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + j], pi[l], acc);
+            }
+            out[j] = -acc + ((j < NX && lane >= 1 && lane <= H) ? pim1[j] : 0.0);
+        }
+    }
+
+    // dyn residual of stage k (lane < H): y_{k+1} - A_k y_k - B_k v_k - c_k for stage vectors y = [x; u]
+    __device__ static void dyn_residual(const Lds& L, int H, int lane, const double (&d)[NB], const double (&c)[NX],
+                                        double (&r)[NX]) {
+        double xn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xn[i] = __shfl(d[i], lane < 63 ? lane + 1 : 63);
+        const double* G = L.G + (size_t)min(lane, H - 1) * NX * NB;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = 0.0;
+            if (lane < H) {
+                acc = xn[i] - c[i];
+#pragma unroll
+                for (int j = 0; j < NB; ++j) acc = fma(-G[i * NB + j], d[j], acc);
+            }
+            r[i] = acc;
+        }
+    }
+
+    __device__ static double max_step(double v, double dv) { return dv < 0.0 ? -v / dv : 1e300; }
+
+    // ------------------------------------------------------------------ the kernel body
+    __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
+        const int H = P.H;
+        const int lane = threadIdx.x;
+        const int b = blockIdx.x;
+        extern __shared__ __attribute__((aligned(16))) double smem[];
+        const Lds L = carve(smem, H);
+        const bool on = lane <= H;
+        const bool act_x = on && lane >= 1;
+        const bool act_u = lane < H;
+        const int k = min(lane, H);
+
+        // ---------------- load instance state (acados memory: iterate + multipliers)
+        double w[NB], lamL[NB], lamU[NB], pi[NX];
+        const double* xg = S.x + (size_t)b * (H + 1) * NX;
+        const double* ug = S.u + (size_t)b * H * NU;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) w[i] = on ? xg[k * NX + i] : 0.0;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) w[NX + a] = act_u ? ug[k * NU + a] : 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pi[i] = act_u ? S.pi[((size_t)b * H + k) * NX + i] : 0.0;
+#pragma unroll
+        for (int v = 0; v < NB; ++v) {
+            const bool av = v < NX ? act_x : act_u;
+            lamL[v] = av ? S.lam[((size_t)b * (H + 1) + k) * 2 * NB + v] : 0.0;
+            lamU[v] = av ? S.lam[((size_t)b * (H + 1) + k) * 2 * NB + NB + v] : 0.0;
+        }
+        double x0[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) x0[i] = io.x0[(size_t)b * NX + i];
+
+        // ---------------- reference window and cost (gpmpc.py:356-361, 231-239)
+        double yr[NB], hd[NB];
+        {
+            const int t = (io.tstep[b] + k) % P.traj_len;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                yr[i] = P.traj[(size_t)t * NX + i];
+                hd[i] = act_x ? (lane < H ? P.cost_scale : 1.0) * P.q[i] : 1.0;
+            }
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                yr[NX + a] = P.u_eq[a];
+                hd[NX + a] = act_u ? P.cost_scale * P.r[a] : 1.0;
+            }
+        }
+
+        // ---------------- constraint tightening from the previous solution (gpmpc.py:425-498)
+        double tsd[NB];  // icdf * sqrt(variance) per stage variable
+#pragma unroll
+        for (int v = 0; v < NB; ++v) tsd[v] = 0.0;
+        if (P.tighten && S.has_prev[b]) {
+            if (lane < H) {
+                double Wt[NUNC][NGP];
+                M::var_weights(w, w + NX, Wt);
+                const double dt2 = P.dt * P.dt;
+#pragma unroll
+                for (int j = 0; j < NUNC; ++j) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int g = 0; g < NGP; ++g)
+                        acc = fma(Wt[j][g], S.var[((size_t)b * H + lane) * NGP + g] + P.gp[g].sn2, acc);
+                    L.cd[lane * NUNC + j] = acc * dt2;
+                }
+            }
+            double* Sig = L.Sig;
+            double* T1 = L.Sig + NX * NX;
+            double* U = L.Sig + 2 * NX * NX;
+            for (int e = lane; e < NX * NX; e += 64) Sig[e] = 0.0;
+            WSYNC();
+            for (int kk = 0; kk <= H; ++kk) {
+                // record sqrt(diag Sigma_k) and sqrt(diag K Sigma_k K')
+                for (int e = lane; e < NX * NX + NU * NX; e += 64) {
+                    if (e < NX * NX) {
+                        const int i = e / NX, j = e % NX;
+                        double acc = 0.0;
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) acc = fma(P.Acl[i * NX + m], Sig[m * NX + j], acc);
+                        T1[e] = acc;
+                    } else {
+                        const int q = e - NX * NX, a = q / NX, j = q % NX;
+                        double acc = 0.0;
+#pragma unroll
+                        for (int m = 0; m < NX; ++m) acc = fma(P.K[a * NX + m], Sig[m * NX + j], acc);
+                        U[q] = acc;
+                    }
+                }
+                if (lane < NX) L.hq[kk * NB + lane] = P.icdf * sqrt(fmax(Sig[lane * NX + lane], 0.0));
+                WSYNC();
+                if (lane < NU) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) acc = fma(U[lane * NX + m], P.K[lane * NX + m], acc);
+                    L.hq[kk * NB + NX + lane] = P.icdf * sqrt(fmax(acc, 0.0));
+                }
+                if (kk == H) break;
+                for (int e = lane; e < NX * NX; e += 64) {
+                    const int i = e / NX, j = e % NX;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NX; ++m) acc = fma(T1[i * NX + m], P.Acl[j * NX + m], acc);
+                    if (i == j) {
+#pragma unroll
+                        for (int q = 0; q < NUNC; ++q)
+                            if (M::unc[q] == i) acc += L.cd[kk * NUNC + q];
+                    }
+                    Sig[e] = acc;
+                }
+                WSYNC();
+            }
+            WSYNC();
+#pragma unroll
+            for (int v = 0; v < NB; ++v) tsd[v] = on ? L.hq[k * NB + v] : 0.0;
+        }
+        if (S.tight != nullptr && on) {
+#pragma unroll
+            for (int v = 0; v < NB; ++v) S.tight[((size_t)b * (H + 1) + k) * NB + v] = tsd[v];
+        }
+        // tightened boxes lo + t - uh <= w <= hi - t + uh   (gpmpc.py:296-314)
+        double lb[NB], ub[NB];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            lb[i] = P.x_lo[i] + tsd[i] - P.uh;
+            ub[i] = P.x_hi[i] - tsd[i] + P.uh;
+        }
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            lb[NX + a] = P.u_lo[a] + tsd[NX + a] - P.uh;
+            ub[NX + a] = P.u_hi[a] - tsd[NX + a] + P.uh;
+        }
+
+        // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
+        const double nc = 2.0 * (double)H * (double)NB;
+        int status = kMaxIter, it = 0, qp_total = 0;
+        double res[4] = {0, 0, 0, 0};
+        for (it = 0;; ++it) {
+            double F[NX];
+            linearize(P, L, H, lane, w, F);
+            WSYNC();
+            // NLP residuals with the current multipliers
+            double ct[NB];
+            ctpi(L, H, lane, pi, ct);
+            double xn[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xn[i] = __shfl(w[i], lane < 63 ? lane + 1 : 63);
+            double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0;
+#pragma unroll
+            for (int v = 0; v < NB; ++v) {
+                const bool av = v < NX ? act_x : act_u;
+                if (av) {
+                    r_stat = fmax(r_stat, fabs(hd[v] * (w[v] - yr[v]) - lamL[v] + lamU[v] + ct[v]));
+                    r_ineq = fmax(r_ineq, fmax(lb[v] - w[v], w[v] - ub[v]));
+                    r_comp = fmax(r_comp, fmax(fabs(lamL[v] * (w[v] - lb[v])), fabs(lamU[v] * (ub[v] - w[v]))));
+                }
+            }
+            double cq[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                cq[i] = act_u ? F[i] - xn[i] : 0.0;
+                r_eq = fmax(r_eq, fabs(cq[i]));
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) r_ineq = fmax(r_ineq, fabs(x0[i] - w[i]));  // lbx = ubx = obs
+            }
+            res[0] = wave_max(r_stat);
+            res[1] = wave_max(r_eq);
+            res[2] = wave_max(r_ineq);
+            res[3] = wave_max(r_comp);
+            if (!(res[0] == res[0] && res[1] == res[1] && res[2] == res[2] && res[3] == res[3])) { status = kNaN; break; }
+            if (res[0] <= P.tol_stat && res[1] <= P.tol_eq && res[2] <= P.tol_ineq && res[3] <= P.tol_comp) {
+                status = kSuccess;
+                break;
+            }
+            if (it == P.max_iter) { status = kMaxIter; break; }
+
+            // ---------------- QP in the step variables (HPIPM's role), Mehrotra IPM
+            double lbd[NB], ubd[NB], g[NB], d[NB], sl[NB], su[NB], ll[NB], lu[NB], piq[NX];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) {
+                const bool av = v < NX ? act_x : act_u;
+                g[v] = av ? hd[v] * (w[v] - yr[v]) : 0.0;
+                lbd[v] = lb[v] - w[v];
+                ubd[v] = ub[v] - w[v];
+                d[v] = (lane == 0 && v < NX) ? x0[v] - w[v] : 0.0;   // dx_0 = e0 fixed
+                sl[v] = av ? fmax(-lbd[v], 1e-2) : 1.0;
+                su[v] = av ? fmax(ubd[v], 1e-2) : 1.0;
+                ll[v] = av ? P.qp_mu0 / sl[v] : 0.0;
+                lu[v] = av ? P.qp_mu0 / su[v] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) piq[i] = 0.0;
+            if (act_u) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) L.cc[lane * NX + i] = 0.0;  // placeholder, set per IPM iteration
+            }
+            bool qp_ok = true;
+            int qit = 0;
+            for (qit = 0; qit < P.qp_max_iter; ++qit) {
+                double rd[NB], rl[NB], ru[NB], rp[NX], ctq[NB];
+                ctpi(L, H, lane, piq, ctq);
+                dyn_residual(L, H, lane, d, cq, rp);
+                double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    rd[v] = av ? fma(hd[v], d[v], g[v]) - ll[v] + lu[v] + ctq[v] : 0.0;
+                    rl[v] = av ? d[v] - lbd[v] - sl[v] : 0.0;
+                    ru[v] = av ? ubd[v] - d[v] - su[v] : 0.0;
+                    m_rd = fmax(m_rd, fabs(rd[v]));
+                    m_lu = fmax(m_lu, fmax(fabs(rl[v]), fabs(ru[v])));
+                    mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
+                const double mu = wave_sum(mu_l) / nc;
+                m_rd = wave_max(m_rd);
+                m_rb = wave_max(m_rb);
+                m_lu = wave_max(m_lu);
+                if (!(mu == mu) || !(m_rd == m_rd)) { qp_ok = false; break; }
+                if (m_rd <= P.qp_tol && m_rb <= P.qp_tol && m_lu <= P.qp_tol && mu <= P.qp_tol) break;
+
+                // Riccati data: hq = H + Sigma, cc = -r_pi ; gq for the predictor
+                double sig[NB];
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    sig[v] = av ? ll[v] / sl[v] + lu[v] / su[v] : 0.0;
+                    if (on) {
+                        L.hq[k * NB + v] = hd[v] + sig[v];
+                        // predictor: r_ml = ll sl, r_mu = lu su
+                        L.gq[k * NB + v] = av ? rd[v] + (ll[v] * sl[v] + ll[v] * rl[v]) / sl[v]
+                                                      - (lu[v] * su[v] + lu[v] * ru[v]) / su[v] : 0.0;
+                    }
+                }
+                if (act_u) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) L.cc[lane * NX + i] = -rp[i];
+                }
+                WSYNC();
+                if (!riccati_factor(L, H, lane)) { qp_ok = false; break; }
+                riccati_forward(L, H, lane);
+                double dd[NB], dp[NX], dsl[NB], dsu[NB], dll[NB], dlu[NB];
+                recover_step(L, H, lane, dd, dp);
+                double amax = 1.0;
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    dsl[v] = av ? dd[v] + rl[v] : 0.0;
+                    dsu[v] = av ? -dd[v] + ru[v] : 0.0;
+                    dll[v] = av ? (-ll[v] * sl[v] - ll[v] * dsl[v]) / sl[v] : 0.0;
+                    dlu[v] = av ? (-lu[v] * su[v] - lu[v] * dsu[v]) / su[v] : 0.0;
+                    if (av) {
+                        amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
+                                               fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                    }
+                }
+                const double a_aff = wave_min(amax);
+                double mua_l = 0.0;
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    if (av)
+                        mua_l += (ll[v] + a_aff * dll[v]) * (sl[v] + a_aff * dsl[v]) +
+                                 (lu[v] + a_aff * dlu[v]) * (su[v] + a_aff * dsu[v]);
+                }
+                const double mu_aff = wave_sum(mua_l) / nc;
+                const double sr = mu_aff / mu;
+                const double sigma = sr * sr * sr;
+                // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu
+                double rml[NB], rmu[NB];
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    rml[v] = av ? ll[v] * sl[v] + dll[v] * dsl[v] - sigma * mu : 0.0;
+                    rmu[v] = av ? lu[v] * su[v] + dlu[v] * dsu[v] - sigma * mu : 0.0;
+                    if (on) L.gq[k * NB + v] = av ? rd[v] + (rml[v] + ll[v] * rl[v]) / sl[v] - (rmu[v] + lu[v] * ru[v]) / su[v] : 0.0;
+                }
+                WSYNC();
+                riccati_vector(L, H, lane);
+                riccati_forward(L, H, lane);
+                recover_step(L, H, lane, dd, dp);
+                amax = 1.0;
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    dsl[v] = av ? dd[v] + rl[v] : 0.0;
+                    dsu[v] = av ? -dd[v] + ru[v] : 0.0;
+                    dll[v] = av ? (-rml[v] - ll[v] * dsl[v]) / sl[v] : 0.0;
+                    dlu[v] = av ? (-rmu[v] - lu[v] * dsu[v]) / su[v] : 0.0;
+                    if (av) {
+                        amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
+                                               fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                    }
+                }
+                const double alpha = fmin(1.0, 0.995 * wave_min(amax));
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    const bool av = v < NX ? act_x : act_u;
+                    if (av) {
+                        d[v] = fma(alpha, dd[v], d[v]);
+                        sl[v] = fma(alpha, dsl[v], sl[v]);
+                        su[v] = fma(alpha, dsu[v], su[v]);
+                        ll[v] = fma(alpha, dll[v], ll[v]);
+                        lu[v] = fma(alpha, dlu[v], lu[v]);
+                    }
+                }
+                if (act_u) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
+                }
+            }
+            qp_total += qit;
+            if (!qp_ok) { status = kQPFailure; break; }
+            // full SQP step: w += d, multipliers <- QP multipliers
+            bool fin = true;
+#pragma unroll
+            for (int v = 0; v < NB; ++v) {
+                const bool av = v < NX ? (act_x || lane == 0) : act_u;
+                if (av) w[v] += d[v];
+                fin = fin && (w[v] == w[v]);
+                const bool ab = v < NX ? act_x : act_u;
+                lamL[v] = ab ? ll[v] : 0.0;
+                lamU[v] = ab ? lu[v] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pi[i] = act_u ? piq[i] : 0.0;
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) w[i] = x0[i];
+            }
+            if (wave_min(fin ? 1.0 : 0.0) < 0.5) { status = kNaN; break; }
+        }
+
+        // ---------------- write back (acados memory + x_prev/u_prev, gpmpc.py:366-368)
+        double* xo = S.x + (size_t)b * (H + 1) * NX;
+        double* uo = S.u + (size_t)b * H * NU;
+        if (on) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) xo[k * NX + i] = w[i];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) {
+                S.lam[((size_t)b * (H + 1) + k) * 2 * NB + v] = lamL[v];
+                S.lam[((size_t)b * (H + 1) + k) * 2 * NB + NB + v] = lamU[v];
+            }
+        }
+        if (act_u) {
+#pragma unroll
+            for (int a = 0; a < NU; ++a) uo[k * NU + a] = w[NX + a];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) S.pi[((size_t)b * H + k) * NX + i] = pi[i];
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int a = 0; a < NU; ++a) io.u0[(size_t)b * NU + a] = w[NX + a];
+            io.status[b] = status;
+            io.sqp_iter[b] = it;
+            io.qp_iter[b] = qp_total;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
+            S.has_prev[b] = 1;
+        }
+    }
+};
+
+}  // namespace gpmpc
+
+namespace gpmpc {
+
+template <int ID>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
+    SqpKernel<ID>::run(P, S, io);
+}
+
+template <int ID>
+hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+    const size_t lds = SqpKernel<ID>::lds_doubles(P.H) * sizeof(double);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(sqp_step_kernel<ID>, dim3(batch), dim3(64), lds, stream, P, S, io);
+    return hipGetLastError();
+}
+
+size_t sqp_lds_bytes(int model, int H) {
+    switch (model) {
+        case kQuad2D: return SqpKernel<kQuad2D>::lds_doubles(H) * sizeof(double);
+        case kQuad3D: return SqpKernel<kQuad3D>::lds_doubles(H) * sizeof(double);
+        case kCartpole: return SqpKernel<kCartpole>::lds_doubles(H) * sizeof(double);
+    }
+    return 0;
+}
+
+hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+    switch (P.model) {
+        case kQuad2D: return launch_sqp_step<kQuad2D>(P, S, io, batch, stream);
+        case kQuad3D: return launch_sqp_step<kQuad3D>(P, S, io, batch, stream);
+        case kCartpole: return launch_sqp_step<kCartpole>(P, S, io, batch, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace gpmpc

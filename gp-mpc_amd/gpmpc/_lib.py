@@ -1,0 +1,84 @@
+"""ctypes binding of the C ABI in ``include/gpmpc_mi355x.h`` (libgpmpc_mi355x.so).
+
+The product path has no CPU fallback: if the HIP library is missing or no GPU is present,
+every entry point raises :class:`GPMPCError`.  torch is imported first so that the library
+binds to the same HIP runtime instance torch uses (same ``libamdhip64.so.7`` soname) and
+torch device pointers / streams are valid on both sides.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_void_p
+from pathlib import Path
+
+import torch  # noqa: F401  (HIP runtime shared with torch)
+
+LIB_PATH = Path(os.environ.get("GPMPC_LIB", Path(__file__).resolve().parent / "lib" / "libgpmpc_mi355x.so"))
+
+_lib = None
+
+# C-ABI symbols and their signatures (restype, argtypes).
+_D = c_double
+_I = c_int32
+_P = c_void_p
+SIGNATURES = {
+    "gpmpc_create": (_I, [_I, _I, _I, _I, POINTER(_P)]),
+    "gpmpc_destroy": (None, [_P]),
+    "gpmpc_last_error": (c_char_p, []),
+    "gpmpc_set_model": (_I, [_P, _P, _I, _D, _P, _P, _P, _P, _P, _P, _P, _D, _I]),
+    "gpmpc_set_reference": (_I, [_P, _P, _I]),
+    "gpmpc_set_options": (_I, [_P, _I, _D, _D, _D, _D, _I, _D, _D]),
+    "gpmpc_set_gp": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _D, _D, _D]),
+    "gpmpc_use_gp": (_I, [_P, _I]),
+    "gpmpc_set_tightening": (_I, [_P, _I, _D, _P, _P, _P]),
+    "gpmpc_reset": (_I, [_P, _I, _I, _P]),
+    "gpmpc_set_iterate": (_I, [_P, _I, _P, _P, _P]),
+    "gpmpc_solve": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "gpmpc_get_solution": (_I, [_P, _I, _P, _P, _P, _P]),
+    "gpmpc_gp_predict": (_I, [_P, _I, _P, _I, _P, _P, _I, _P]),
+    "gpmpc_gp_posterior": (_I, [_I, _I, _I, _P, _P, _D, _D, _D, _P, _I, _P, _P, _I, _P]),
+    "gpmpc_plant_step": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "gpmpc_lds_bytes": (c_int64, [_I, _I]),
+}
+
+
+class GPMPCError(RuntimeError):
+    pass
+
+
+def load(require_gpu: bool = True):
+    """Load the HIP library (raises GPMPCError if it is missing; optionally if no GPU)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise GPMPCError(f"HIP extension not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+        lib = ctypes.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise GPMPCError("no HIP device available: the GP-MPC path runs only on the GPU (no CPU fallback)")
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != 0:
+        msg = _lib.gpmpc_last_error().decode() if _lib is not None else "library not loaded"
+        raise GPMPCError(f"gpmpc C-ABI error {status}: {msg}")
+
+
+def ptr(t) -> int | None:
+    """Raw pointer of a tensor / numpy array (None passes NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

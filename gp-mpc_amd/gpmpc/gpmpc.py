@@ -1,0 +1,213 @@
+"""GP-MPC controller on the MI355X (drop-in for ``gpmpc/gpmpc.py``).
+
+:class:`GPMPC` keeps the reference's surface -- ``GPMPC(model, traj, prior_params, horizon,
+q_mpc, r_mpc, sparse_gp, prob, max_gp_samples, seed, device)``, ``train_gp``, ``reset``,
+``select_action(obs) -> action``, ``x_prev`` / ``u_prev``, ``prior_ctrl``,
+``gaussian_process`` (`gpmpc/gpmpc.py:20-111,153-164,334-368`) -- and adds the batched
+form ``select_action_batch(obs[B, nx]) -> actions[B, nu]`` on device tensors.  The
+acados OCP (`gpmpc/gpmpc.py:166-320`) is replaced by the batched HIP solver
+(``csrc/sqp_kernel.hip``); there is no code generation and no CPU fallback.
+
+``model`` is a :class:`gpmpc.models.ModelSpec` or its name (``"quad3d"``, ``"quad2d"``,
+``"cartpole"``); it takes the role of crazyflow's ``symbolic_attitude`` model object.
+"""
+
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import _lib
+from .gp import GaussianProcess, fit_gp
+from .models import ModelSpec, get_spec
+from .mpc import MPC
+from .solver import BatchSolver, STATUS_NAMES, inverse_cdf, setup_prior_dynamics
+
+
+class GPMPC:
+    """Implements a GP-MPC controller on the MI355X HIP solver."""
+
+    def __init__(self, symbolic_model, traj: np.ndarray | None = None, prior_params: dict | None = None,
+                 horizon: int = 25, q_mpc: list | None = None, r_mpc: list | None = None, sparse_gp: bool = False,
+                 prob: float = 0.955, max_gp_samples: int = 30, seed: int = 1337, device: str = "cuda",
+                 output_dir: Path | None = None, batch: int = 1, **solver_kw):
+        spec = symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)
+        self.model = spec
+        if q_mpc is not None:
+            spec.q_diag = np.asarray(q_mpc, dtype=np.float64)
+        if r_mpc is not None:
+            spec.r_diag = np.asarray(r_mpc, dtype=np.float64)
+        assert len(spec.q_diag) == spec.nx and len(spec.r_diag) == spec.nu
+        if prior_params is not None:
+            missing = [k for k in spec.prior if k not in prior_params]
+            if missing:
+                raise ValueError(f"GPMPC requires prior_params with keys {sorted(spec.prior)}; missing {missing}")
+            spec.prior = {k: float(prior_params[k]) for k in spec.prior}
+        self.sparse = sparse_gp
+        self.output_dir = output_dir
+        self.device = torch.device(device)
+        self.dt = spec.dt
+        self.T = int(horizon)
+        self.Q, self.R = np.diag(spec.q_diag), np.diag(spec.r_diag)
+        self.traj = spec.reference_trajectory() if traj is None else np.asarray(traj, dtype=np.float64)
+        self.ref_action = np.repeat(spec.u_eq[:, None], self.T, axis=1)
+        self.traj_step = 0
+        self.np_random = np.random.default_rng(seed)
+        self.gp_idx = self._gp_columns(spec)
+        self.gaussian_process: list[GaussianProcess] | None = None
+        self._requires_recompile = False
+        self.prob = prob
+        self.inverse_cdf = inverse_cdf(prob, spec.nx)
+        self.max_gp_samples = max_gp_samples
+        self.Bd = spec.bd_matrix()
+        self.batch = int(batch)
+
+        self.prior_ctrl = MPC(spec, traj=self.traj, horizon=self.T, q_mpc=list(spec.q_diag),
+                              r_mpc=list(spec.r_diag), device=device, batch=batch, **solver_kw)
+        dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
+        self.discrete_dfdx, self.discrete_dfdu, self.lqr_gain = setup_prior_dynamics(dfdx, dfdu, self.Q, self.R, self.dt)
+
+        self.solver = BatchSolver(spec, self.T, self.batch, device=self.device, traj=self.traj, uh=-1e-8, **solver_kw)
+        self.solver.set_tightening(True, prob, self.discrete_dfdx, self.discrete_dfdu, self.lqr_gain)
+        self._x_prev = None
+        self._u_prev = None
+        self._has_prev = False
+        self._tstep = torch.zeros(self.batch, dtype=torch.int32, device=self.device)
+
+    @staticmethod
+    def _gp_columns(spec: ModelSpec) -> list[list[int]]:
+        """Column groups of the concatenated GP training inputs (`gpmpc/gpmpc.py:59`)."""
+        cols, c = [], 0
+        for d in spec.gp_dims:
+            cols.append(list(range(c, c + d)))
+            c += d
+        return cols
+
+    # ------------------------------------------------------------------ GP management
+    def train_gp(self, x: np.ndarray, y: np.ndarray, lr: float, iterations: int):
+        """Fit one GP per output column on its input columns (`gpmpc/gpmpc.py:153-164`)."""
+        x_train = torch.tensor(np.asarray(x, dtype=np.float64))
+        y_train = torch.tensor(np.asarray(y, dtype=np.float64))
+        gps = []
+        for i, idx in enumerate(self.gp_idx):
+            gp = GaussianProcess(x_train[:, idx], y_train[:, i])
+            fit_gp(gp, n_train=iterations, lr=lr, device="cpu")
+            gps.append(gp)
+        self.set_gaussian_processes(gps)
+
+    def set_gaussian_processes(self, gps: list[GaussianProcess]):
+        for gp in gps:
+            if gp.K is None:
+                gp.K, gp.K_inv = gp.compute_covariances()
+        self.gaussian_process = gps
+        self._requires_recompile = True
+
+    def precompute_sparse_posterior_mean(self, n_samples: int):
+        """FITC weights on random training rows (`gpmpc/gpmpc.py:377-400`)."""
+        gps = self.gaussian_process
+        n = gps[0].train_inputs[0].shape[0]
+        rand_idx = self.np_random.choice(range(n), size=n_samples, replace=False)
+        out = []
+        for gp in gps:
+            X = gp.train_inputs[0].cpu()
+            y = gp.train_targets.cpu()
+            S = X[rand_idx]
+            with torch.no_grad():
+                K = gp.K.cpu()
+                K_ss = gp.kernel(S)
+                K_xs = gp.kernel(X, S)
+                Gamma = torch.diagonal(K - K_xs @ torch.linalg.solve(K_ss, K_xs.T))
+                Gamma_inv = torch.diag_embed(1 / Gamma)
+                Sigma_inv = K_ss + K_xs.T @ Gamma_inv @ K_xs
+                w = torch.linalg.solve(Sigma_inv, K_xs.T) @ Gamma_inv @ y
+            # the solver evaluates sf2 * sum_j w_j exp(.): the reference's covSE already carries sf2
+            out.append((S.numpy(), w.numpy()))
+        return out
+
+    # ------------------------------------------------------------------ control
+    def reset(self):
+        """Reset before running (`gpmpc/gpmpc.py:94-111`): upload new GPs, forget x_prev/u_prev."""
+        self.traj_step = 0
+        self._tstep.zero_()
+        if self._requires_recompile:
+            assert self.gaussian_process is not None, "GP must be trained before reinitializing"
+            fitc = None
+            if self.sparse:
+                n = self.gaussian_process[0].train_targets.shape[0]
+                fitc = self.precompute_sparse_posterior_mean(min(n, self.max_gp_samples))
+            self.solver.set_gps(self.gaussian_process, with_variance=True, fitc=fitc)
+            self._requires_recompile = False
+        self.solver.reset(reset_iterate=False)  # acados keeps its memory (gpmpc.py:94-111)
+        self._x_prev = None
+        self._u_prev = None
+        self._has_prev = False
+
+    @property
+    def x_prev(self):
+        if not self._has_prev:
+            return None
+        if self._x_prev is None:
+            x, u, _ = self.solver.solution()
+            self._x_prev = x[0].T.cpu().numpy() if self.batch == 1 else x.cpu().numpy()
+            self._u_prev = u[0].T.cpu().numpy() if self.batch == 1 else u.cpu().numpy()
+        return self._x_prev
+
+    @property
+    def u_prev(self):
+        if not self._has_prev:
+            return None
+        _ = self.x_prev
+        return self._u_prev
+
+    def select_action(self, obs: np.ndarray) -> np.ndarray:
+        """Solve the nonlinear MPC problem to get the next action (`gpmpc/gpmpc.py:334-368`)."""
+        assert not self._requires_recompile, "GP model must be uploaded (call reset())"
+        assert self.gaussian_process is not None, "Gaussian processes are not initialized"
+        assert self.batch == 1, "select_action is the single-instance form; use select_action_batch"
+        x0 = torch.as_tensor(np.asarray(obs, dtype=np.float64).reshape(1, -1), device=self.device)
+        self._tstep.fill_(self.traj_step)
+        self.traj_step += 1
+        u0 = self.solver.solve(x0, self._tstep)
+        status = int(self.solver.status[0].item())
+        assert status in [0, 2], f"solver returned unexpected status {status} ({STATUS_NAMES.get(status)})."
+        self._has_prev = True
+        self._x_prev = self._u_prev = None
+        return u0[0].cpu().numpy()
+
+    def select_action_batch(self, obs: torch.Tensor, tstep: torch.Tensor | None = None, check: bool = False):
+        """Batched select_action on device tensors: obs (B, nx) float64 -> actions (B, nu).
+
+        ``tstep`` (B,) int32 gives each instance's reference index (default: the shared
+        ``traj_step`` counter).  ``check=True`` synchronises and asserts status in {0, 2}.
+        """
+        assert not self._requires_recompile, "GP model must be uploaded (call reset())"
+        if tstep is None:
+            self._tstep.fill_(self.traj_step)
+            tstep = self._tstep
+            self.traj_step += 1
+        u0 = self.solver.solve(obs, tstep)
+        self._has_prev = True
+        self._x_prev = self._u_prev = None
+        if check:
+            bad = ~((self.solver.status == 0) | (self.solver.status == 2))
+            if bool(bad.any()):
+                i = int(torch.nonzero(bad)[0])
+                raise AssertionError(f"instance {i}: unexpected status {int(self.solver.status[i])}")
+        return u0
+
+    def reference_trajectory(self) -> np.ndarray:
+        """`gpmpc/gpmpc.py:509-514`."""
+        indices = np.arange(self.traj_step, self.traj_step + self.T + 1) % self.traj.shape[-1]
+        return self.traj[:, indices]
+
+    @staticmethod
+    def setup_constraints(sym, low, high):
+        """Rows A sym - b of the box constraints (`gpmpc/gpmpc.py:327-332`)."""
+        dim = low.shape[0]
+        A = np.vstack((-np.eye(dim), np.eye(dim)))
+        b = np.hstack((-low, high))
+        return A @ sym - b
+
+    setup_prior_dynamics = staticmethod(setup_prior_dynamics)

@@ -1,0 +1,187 @@
+"""Batched solver handle: B independent GP-MPC instances on one MI355X.
+
+Thin host layer over the C ABI (``include/gpmpc_mi355x.h``): it owns the solver handle,
+uploads the OCP definition and the GP replicas, and runs one batched control step per
+:meth:`BatchSolver.solve` (one ``gpmpc_solve`` call = the variance kernel + the SQP kernel,
+asynchronous on torch's current stream).  All per-step tensors stay on the device.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.linalg
+import scipy.stats
+import torch
+
+from . import _lib
+from .gp import GaussianProcess
+from .models import ModelSpec
+
+STATUS_NAMES = {0: "SUCCESS", 1: "NAN_DETECTED", 2: "MAXITER", 3: "MINSTEP", 4: "QP_FAILURE"}
+
+
+def discretize_linear_system(A, B, dt: float, exact: bool = False):
+    """(Exact) ZOH discretisation (`gpmpc/gpmpc.py:517-527`)."""
+    nx, nu = A.shape[1], B.shape[1]
+    if exact:
+        M = np.zeros((nx + nu, nx + nu))
+        M[:nx, :nx] = A
+        M[:nx, nx:] = B
+        Md = scipy.linalg.expm(M * dt)
+        return Md[:nx, :nx], Md[:nx, nx:]
+    return np.eye(nx) + A * dt, B * dt
+
+
+def setup_prior_dynamics(dfdx, dfdu, Q, R, dt):
+    """LQR gain of the discretised prior (`gpmpc/gpmpc.py:500-507`)."""
+    A, B = discretize_linear_system(dfdx, dfdu, dt, exact=True)
+    P = scipy.linalg.solve_discrete_are(A, B, Q, R)
+    btp = B.T @ P
+    lqr_gain = -np.linalg.inv(R + btp @ B) @ (btp @ A)
+    return A, B, lqr_gain
+
+
+def inverse_cdf(prob: float, nx: int) -> float:
+    """`gpmpc/gpmpc.py:63-65`."""
+    return float(scipy.stats.norm.ppf(1 - (1 / nx - (prob + 1) / (2 * nx))))
+
+
+def _c(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+class BatchSolver:
+    """One solver handle for ``batch`` instances of ``spec`` with horizon ``horizon``."""
+
+    def __init__(self, spec: ModelSpec, horizon: int, batch: int, device="cuda", prior_params: dict | None = None,
+                 traj: np.ndarray | None = None, uh: float = -1e-8, cost_scaling: bool = True, max_iter: int = 25,
+                 tol: float = 1e-6, qp_max_iter: int = 100, qp_tol: float = 1e-10, qp_mu0: float = 1.0):
+        self.lib = _lib.load()
+        self.spec = spec
+        self.H = int(horizon)
+        self.batch = int(batch)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise _lib.GPMPCError("BatchSolver runs on the GPU (device must be cuda)")
+        self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", self.dev_index)
+        self.nx, self.nu = spec.nx, spec.nu
+        h = ctypes.c_void_p()
+        _lib.check(self.lib.gpmpc_create(spec.model_id, self.H, self.batch, self.dev_index, ctypes.byref(h)))
+        self._h = h
+        self.prior = dict(spec.prior if prior_params is None else {**spec.prior, **prior_params})
+        params = _c(spec.param_vector(self.prior))
+        self._keep = [params]
+        _lib.check(self.lib.gpmpc_set_model(
+            self._h, params.ctypes.data, params.size, spec.dt, _c(spec.x_lo).ctypes.data, _c(spec.x_hi).ctypes.data,
+            _c(spec.u_lo).ctypes.data, _c(spec.u_hi).ctypes.data, _c(spec.q_diag).ctypes.data,
+            _c(spec.r_diag).ctypes.data, _c(spec.u_eq).ctypes.data, float(uh), int(cost_scaling)))
+        self.set_options(max_iter=max_iter, tol=tol, qp_max_iter=qp_max_iter, qp_tol=qp_tol, qp_mu0=qp_mu0)
+        self.set_reference(spec.reference_trajectory() if traj is None else traj)
+        self.gps: list[GaussianProcess] | None = None
+        # per-step device buffers
+        kw = dict(device=self.device)
+        B = self.batch
+        self.u0 = torch.zeros(B, self.nu, dtype=torch.float64, **kw)
+        self.status = torch.zeros(B, dtype=torch.int32, **kw)
+        self.sqp_iter = torch.zeros(B, dtype=torch.int32, **kw)
+        self.qp_iter = torch.zeros(B, dtype=torch.int32, **kw)
+        self.res = torch.zeros(B, 4, dtype=torch.float64, **kw)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.gpmpc_destroy(h)
+            self._h = None
+
+    # ------------------------------------------------------------------ configuration
+    def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=100, qp_tol=1e-10, qp_mu0=1.0):
+        _lib.check(self.lib.gpmpc_set_options(self._h, int(max_iter), tol, tol, tol, tol, int(qp_max_iter), qp_tol, qp_mu0))
+
+    def set_reference(self, traj: np.ndarray):
+        traj = _c(traj)
+        if traj.ndim != 2 or traj.shape[0] != self.nx:
+            raise ValueError(f"reference trajectory must be (nx={self.nx}, L)")
+        self.traj = traj
+        _lib.check(self.lib.gpmpc_set_reference(self._h, traj.ctypes.data, traj.shape[1]))
+
+    def set_gps(self, gps: list[GaussianProcess] | None, with_variance: bool = True, fitc: list | None = None):
+        """Upload GP replicas.  ``fitc[g] = (S (M,d), w (M,))`` replaces GP g's mean by the FITC
+        approximation (the variance stays exact, as in `gpmpc/gpmpc.py:441-445`)."""
+        if gps is None:
+            _lib.check(self.lib.gpmpc_use_gp(self._h, 0))
+            self.gps = None
+            return
+        if len(gps) != self.spec.n_gp:
+            raise ValueError(f"{self.spec.name} needs {self.spec.n_gp} GPs")
+        for g, gp in enumerate(gps):
+            lay = gp.device_layout("cpu")
+            X = _c(gp.train_inputs[0].cpu().numpy())
+            Linv = _c(lay["Linv"].cpu().numpy()) if with_variance else None
+            if fitc is not None and fitc[g] is not None:
+                S, w = _c(fitc[g][0]), _c(fitc[g][1])
+                _lib.check(self.lib.gpmpc_set_gp(self._h, g, S.shape[0], S.shape[1], S.ctypes.data, w.ctypes.data,
+                                                 X.shape[0], X.ctypes.data, None if Linv is None else Linv.ctypes.data,
+                                                 gp.lengthscale, gp.outputscale, gp.noise))
+            else:
+                alpha = _c(lay["alpha"].cpu().numpy())
+                _lib.check(self.lib.gpmpc_set_gp(self._h, g, X.shape[0], X.shape[1], X.ctypes.data, alpha.ctypes.data,
+                                                 0, None, None if Linv is None else Linv.ctypes.data,
+                                                 gp.lengthscale, gp.outputscale, gp.noise))
+        _lib.check(self.lib.gpmpc_use_gp(self._h, 1))
+        self.gps = gps
+
+    def set_tightening(self, enabled: bool, prob: float = 0.95, Ad=None, Bd=None, K=None):
+        if not enabled:
+            _lib.check(self.lib.gpmpc_set_tightening(self._h, 0, 0.0, None, None, None))
+            return
+        Ad, Bd, K = _c(Ad), _c(Bd), _c(K)
+        self._keep += [Ad, Bd, K]
+        _lib.check(self.lib.gpmpc_set_tightening(self._h, 1, inverse_cdf(prob, self.nx), Ad.ctypes.data,
+                                                 Bd.ctypes.data, K.ctypes.data))
+
+    # ------------------------------------------------------------------ stepping
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def reset(self, reset_iterate: bool = False):
+        _lib.check(self.lib.gpmpc_reset(self._h, self.batch, int(reset_iterate), self._stream()))
+
+    def set_iterate(self, x: torch.Tensor, u: torch.Tensor):
+        x = x.to(self.device, torch.float64).contiguous()
+        u = u.to(self.device, torch.float64).contiguous()
+        assert x.shape == (self.batch, self.H + 1, self.nx) and u.shape == (self.batch, self.H, self.nu)
+        _lib.check(self.lib.gpmpc_set_iterate(self._h, self.batch, x.data_ptr(), u.data_ptr(), self._stream()))
+        torch.cuda.current_stream(self.device).synchronize()
+
+    def solve(self, x0: torch.Tensor, tstep: torch.Tensor) -> torch.Tensor:
+        """One batched select_action: returns u0 (B, nu); status etc. in the buffers."""
+        if x0.shape != (self.batch, self.nx) or x0.dtype != torch.float64 or x0.device != self.device:
+            raise ValueError(f"x0 must be a ({self.batch}, {self.nx}) float64 tensor on {self.device}")
+        if tstep.shape != (self.batch,) or tstep.dtype != torch.int32 or tstep.device != self.device:
+            raise ValueError(f"tstep must be a ({self.batch},) int32 tensor on {self.device}")
+        x0 = x0.contiguous()
+        _lib.check(self.lib.gpmpc_solve(self._h, self.batch, x0.data_ptr(), tstep.data_ptr(), self.u0.data_ptr(),
+                                        self.status.data_ptr(), self.sqp_iter.data_ptr(), self.qp_iter.data_ptr(),
+                                        self.res.data_ptr(), self._stream()))
+        return self.u0
+
+    def solution(self):
+        x = torch.empty(self.batch, self.H + 1, self.nx, dtype=torch.float64, device=self.device)
+        u = torch.empty(self.batch, self.H, self.nu, dtype=torch.float64, device=self.device)
+        t = torch.empty(self.batch, self.H + 1, self.nx + self.nu, dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.gpmpc_get_solution(self._h, self.batch, x.data_ptr(), u.data_ptr(), t.data_ptr(),
+                                               self._stream()))
+        return x, u, t
+
+    def plant_step(self, x: torch.Tensor, u: torch.Tensor, tstep: torch.Tensor | None = None,
+                   params: dict | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Synthetic plant: RK4 of the prior-form model with ``params`` (default: spec.true_params)."""
+        p = _c(self.spec.param_vector(self.spec.true_params if params is None else params))
+        out = torch.empty_like(x) if out is None else out
+        _lib.check(self.lib.gpmpc_plant_step(self._h, x.shape[0], p.ctypes.data, x.data_ptr(), u.data_ptr(),
+                                             out.data_ptr(), None if tstep is None else tstep.data_ptr(),
+                                             self._stream()))
+        return out

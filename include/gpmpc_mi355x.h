@@ -1,0 +1,145 @@
+/* C ABI of the MI355X-native GP-MPC solve path (gfx950).
+ *
+ * This is the drop-in boundary for the reference's hot path.  Each entry point names the
+ * reference interface it replaces (file:line in amacati/gp-mpc).  All device pointers are
+ * plain HIP device allocations (e.g. torch tensors' data_ptr()); host pointers are noted.
+ * Calls are asynchronous on the given stream (NULL = default stream) unless noted.
+ * No C++ exceptions cross this boundary; every call returns a gpmpc_status and
+ * gpmpc_last_error() describes the last failure of the calling thread.
+ *
+ * Threading: one handle per GPU/process, driven by one host thread at a time
+ * (the reference drives one acados solver from one Python thread, gpmpc/gpmpc.py:105-107).
+ */
+#ifndef GPMPC_MI355X_H
+#define GPMPC_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gpmpc_handle gpmpc_handle;
+
+typedef enum {
+    GPMPC_OK = 0,
+    GPMPC_ERR_ARG = -1,     /* invalid argument / shape */
+    GPMPC_ERR_HIP = -2,     /* HIP runtime error (message in gpmpc_last_error) */
+    GPMPC_ERR_STATE = -3,   /* call out of order (e.g. solve before set_model) */
+    GPMPC_ERR_NOMEM = -4
+} gpmpc_status;
+
+/* Model ids (gpmpc/models.py MODEL_*). */
+enum { GPMPC_MODEL_QUAD2D = 0, GPMPC_MODEL_QUAD3D = 1, GPMPC_MODEL_CARTPOLE = 2 };
+
+/* Per-instance solver status codes, identical to acados (asserted in {0,2} at
+ * gpmpc/gpmpc.py:365 and gpmpc/mpc.py:270). */
+enum { GPMPC_SUCCESS = 0, GPMPC_NAN = 1, GPMPC_MAXITER = 2, GPMPC_MINSTEP = 3, GPMPC_QP_FAILURE = 4 };
+
+/* Create a solver for `max_batch` independent instances of model `model_id` with horizon
+ * `horizon` on HIP device `device`.
+ * Replaces: AcadosOcpSolver(ocp, json) construction at gpmpc/gpmpc.py:105-107 and
+ * gpmpc/mpc.py:143 (code generation + compile there; nothing to compile here). */
+gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, int32_t device, gpmpc_handle** out);
+void gpmpc_destroy(gpmpc_handle* h);
+const char* gpmpc_last_error(void);
+
+/* OCP definition (host arrays, float64).
+ * Replaces: setup_acados_model / setup_acados_optimizer / setup_acados_constraints,
+ * gpmpc/gpmpc.py:166-320 (and gpmpc/mpc.py:150-255).
+ *   params      prior parameters in the model's order (gpmpc/models.py param_vector)
+ *   x_lo..u_hi  box bounds (gpmpc/gpmpc.py:242-246)
+ *   q_diag, r_diag  LINEAR_LS weights W = blkdiag(Q,R), W_e = Q (gpmpc/gpmpc.py:233-234)
+ *   u_eq        input reference (ref_action, gpmpc/gpmpc.py:54)
+ *   uh          upper bound of h = A[x;u] - b - t: -1e-8 GPMPC (gpmpc.py:309-314), +1e-8 MPC
+ *   cost_scaling 1: stage costs scaled by dt, terminal by 1 (acados time-step scaling) */
+gpmpc_status gpmpc_set_model(gpmpc_handle* h, const double* params, int32_t n_params, double dt,
+                             const double* x_lo, const double* x_hi, const double* u_lo, const double* u_hi,
+                             const double* q_diag, const double* r_diag, const double* u_eq, double uh,
+                             int32_t cost_scaling);
+
+/* Periodic reference trajectory (host, shape (nx, L) row-major like the reference's
+ * traj array).  Replaces: GPMPC.reference_trajectory, gpmpc/gpmpc.py:509-514. */
+gpmpc_status gpmpc_set_reference(gpmpc_handle* h, const double* traj_nx_by_L, int32_t L);
+
+/* SQP / QP options.  Reference: nlp_solver_max_iter = 25 (gpmpc/gpmpc.py:262); acados
+ * default NLP tolerances 1e-6.  The QP options belong to the batched IPM. */
+gpmpc_status gpmpc_set_options(gpmpc_handle* h, int32_t max_iter, double tol_stat, double tol_eq,
+                               double tol_ineq, double tol_comp, int32_t qp_max_iter, double qp_tol, double qp_mu0);
+
+/* Load GP `gp_id` (host arrays).
+ *   Mean:      inputs X [n][d] (d <= 3) and weights alpha [n]: m(z) = sf2 sum_i alpha_i e(z, X_i).
+ *              Exact GP: alpha = K^-1 y (gpytorch_predict2casadi, gpmpc/gp.py:72-85).
+ *              FITC: X = inducing inputs, alpha = posterior weights (gpmpc/gpmpc.py:175-187,377-400).
+ *   Variance:  training inputs Xv [nv][d] (NULL -> Xv = X, nv = n) and Linv = inverse Cholesky
+ *              factor of K(Xv,Xv) + noise I [nv][nv] (row-major lower; NULL -> no variance).
+ *              The reference takes the variance from the exact GP even in FITC mode
+ *              (gpmpc/gpmpc.py:441-445).
+ *   lengthscale (isotropic), outputscale, noise: ScaleKernel(RBFKernel()) + Gaussian likelihood. */
+gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, const double* X,
+                          const double* alpha, int32_t nv, const double* Xv, const double* Linv,
+                          double lengthscale, double outputscale, double noise);
+
+/* Enable (1) / disable (0) the GP residual in the dynamics: 0 = nominal MPC
+ * (gpmpc/mpc.py, prior dynamics only). */
+gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled);
+
+/* Constraint tightening (gpmpc/gpmpc.py:425-498): inverse_cdf (gpmpc.py:63-65) and the
+ * prior LQR closed loop: Ad [nx][nx], Bd [nx][nu], K [nu][nx] (gpmpc.py:500-507).
+ * enabled = 0 disables tightening (nominal MPC). */
+gpmpc_status gpmpc_set_tightening(gpmpc_handle* h, int32_t enabled, double inverse_cdf, const double* Ad,
+                                  const double* Bd, const double* K);
+
+/* Forget the previous solution for instances [0, batch): the next solve runs without
+ * tightening (GPMPC.reset, gpmpc/gpmpc.py:109-111).  reset_iterate = 1 also zeroes the
+ * warm-start iterate and multipliers (acados_solver.reset(), gpmpc/mpc.py:147). */
+gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, void* stream);
+
+/* Set the warm-start iterate (device arrays x [B][H+1][nx], u [B][H][nu]); multipliers zeroed. */
+gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_dev, const double* u_dev, void* stream);
+
+/* One batched control step: GPMPC.select_action(obs) for every instance
+ * (gpmpc/gpmpc.py:334-368): tightening from the stored previous solution, SQP to
+ * convergence warm-started from it, store the new solution.
+ *   x0      [B][nx]  initial states (obs)                                   (device)
+ *   tstep   [B]      reference index per instance (traj_step)               (device)
+ *   u0      [B][nu]  first input (return value of select_action)            (device, out)
+ *   status  [B]      acados status code                                     (device, out)
+ *   sqp_iter, qp_iter [B]  SQP iterations / total IPM iterations            (device, out, may be NULL)
+ *   res     [B][4]   final NLP residuals stat, eq, ineq, comp               (device, out, may be NULL) */
+gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const int32_t* tstep, double* u0,
+                         int32_t* status, int32_t* sqp_iter, int32_t* qp_iter, double* res, void* stream);
+
+/* Copy the current solution (x_prev / u_prev, gpmpc/gpmpc.py:366-367) into device arrays
+ * x [B][H+1][nx], u [B][H][nu]; tight [B][H+1][nx+nu] receives the last tightening
+ * magnitudes (icdf*sqrt(var)) if non-NULL. */
+gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, double* u_dev, double* tight_dev,
+                                void* stream);
+
+/* GP posterior at P points Z [P][d] (device): mean [P] and/or variance [P] (either may be
+ * NULL; variance needs Linv).  with_noise = 1 adds the likelihood noise
+ * (gp.likelihood(gp(z)), gpmpc/gpmpc.py:444).  GaussianProcess.predict() of the build. */
+gpmpc_status gpmpc_gp_predict(gpmpc_handle* h, int32_t gp_id, const double* Z, int32_t P, double* mean,
+                              double* var, int32_t with_noise, void* stream);
+
+/* Handle-free GP posterior (GaussianProcess.predict() of the build): GP data already on the
+ * device in the kernel layout -- rows [npad][4] = (x0, x1, x2 zero padded, alpha) and
+ * linvT [npad][npad] = (L^-1)^T zero padded (NULL -> mean only), npad = n rounded up to 16.
+ * Replaces the gpytorch posterior of gpmpc/gpmpc.py:441-445 and the casadi mean export
+ * gpmpc/gp.py:72-85. */
+gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double* rows, const double* linvT,
+                                double lengthscale, double outputscale, double noise, const double* Z, int32_t P,
+                                double* mean, double* var, int32_t with_noise, void* stream);
+
+/* Synthetic plant: x_next = RK4(prior-form dynamics with `params`, no GP) for B instances,
+ * tstep += 1 if tstep != NULL (crazyflow env.step replacement, scripts/run_gp_mpc.py:59). */
+gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* params, const double* x,
+                              const double* u, double* x_next, int32_t* tstep, void* stream);
+
+/* LDS bytes one instance's workgroup needs (capacity planning / tests). */
+int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

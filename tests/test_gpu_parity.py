@@ -1,0 +1,138 @@
+"""HIP path vs CPU oracle on identical seeded inputs (MI355X only).
+
+Tolerances (float64 everywhere):
+* GP mean: |m_gpu - m_cpu| <= 1e-10 * (sf2 * sum|alpha|)   (summation order only)
+* GP variance: |v_gpu - v_cpu| <= 1e-9 * sf2              (explicit L^-1 vs triangular solve)
+* SQP solutions, both solved to KKT tolerance 1e-9: |x_gpu - x_cpu| <= 1e-6 (1 + |x_cpu|).
+  The oracle solves its QPs on the dense KKT system, the GPU by Riccati recursions, so
+  agreement is at the converged NLP solution, not iterate by iterate.
+"""
+
+import numpy as np
+import pytest
+
+from helpers import O, initial_states, lqr, oracle_gps, oracle_step, problem, product_gps
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("name,N", [("quad2d", 200), ("cartpole", 50), ("quad3d", 100), ("quad2d", 1000)])
+def test_gp_predict_matches_oracle(name, N):
+    torch = _torch()
+    spec, data, hyp = problem(name, N)
+    gpo = oracle_gps(data, hyp)
+    gpp = product_gps(data, hyp)
+    rng = np.random.default_rng(7)
+    for g in range(spec.n_gp):
+        X = data[g][0]
+        Z = X[rng.integers(0, N, 300)] + 0.3 * rng.standard_normal((300, X.shape[1]))
+        Z = np.vstack([Z, X[:5]])  # points on the training set: variance ~ noise
+        m, v = gpp[g].predict(torch.tensor(Z, device="cuda"), with_noise=True)
+        m, v = m.cpu().numpy(), v.cpu().numpy()
+        mo = gpo[g].mean(Z)
+        vo = gpo[g].var(Z, with_noise=True)
+        scale = gpo[g].sf2 * np.abs(gpo[g].alpha).sum()
+        assert np.abs(m - mo).max() <= 1e-10 * scale, (g, np.abs(m - mo).max(), scale)
+        assert np.abs(v - vo).max() <= 1e-9 * gpo[g].sf2, (g, np.abs(v - vo).max())
+
+
+def test_gp_predict_edge_cases():
+    torch = _torch()
+    spec, data, hyp = problem("quad2d", 17)  # n not a multiple of 16: padded rows
+    gpp = product_gps(data, hyp)
+    gpo = oracle_gps(data, hyp)
+    m, v = gpp[1].predict(torch.zeros(0, 3, dtype=torch.float64, device="cuda"))
+    assert m.shape == (0,) and v.shape == (0,)
+    Z = np.array([[0.1, -0.2, 0.05]])
+    m, v = gpp[1].predict(torch.tensor(Z, device="cuda"), with_noise=False)
+    np.testing.assert_allclose(m.cpu().numpy(), gpo[1].mean(Z), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(v.cpu().numpy(), gpo[1].var(Z, with_noise=False), rtol=1e-8, atol=1e-12)
+    far = np.array([[1e3, 1e3, 1e3]])  # far from the data: mean 0, variance sf2
+    m, v = gpp[1].predict(torch.tensor(far, device="cuda"), with_noise=False)
+    assert abs(float(m[0])) < 1e-12 and abs(float(v[0]) - hyp[1][1]) < 1e-12
+
+
+@pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 4, 3), ("cartpole", 50, 20, 3, 3),
+                                               ("quad3d", 60, 15, 2, 2)])
+def test_closed_loop_parity(name, N, H, B, steps):
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(name, N)
+    gpo = oracle_gps(data, hyp)
+    gpp = product_gps(data, hyp)
+    mats = lqr(spec)
+    tol = 1e-9
+    solver = BatchSolver(spec, H, B, tol=tol)
+    solver.set_gps(gpp)
+    solver.set_tightening(True, 0.95, *mats)
+    solver.reset(reset_iterate=True)
+    sd = spec.to_dict()
+    opts = O.SQPOptions(tol_stat=tol, tol_eq=tol, tol_ineq=tol, tol_comp=tol, qp_tol=1e-11)
+    orc = [O.SQPSolver(sd, O.Dynamics(sd, gpo), H, opts) for _ in range(B)]
+    plant = O.Dynamics(sd, None, params=spec.true_params)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, B)
+    prev = [None] * B
+    for step in range(steps):
+        xt = torch.tensor(x0, device="cuda")
+        ts = torch.tensor(phase + step, dtype=torch.int32, device="cuda")
+        u0 = solver.solve(xt, ts).cpu().numpy()
+        st = solver.status.cpu().numpy()
+        xs, us, tight = (a.cpu().numpy() for a in solver.solution())
+        for b in range(B):
+            so, sc, ic = oracle_step(spec, orc[b], gpo, x0[b], phase[b] + step, H, traj, prev[b], lqr_mats=mats)
+            assert st[b] == so == 0, (step, b, st[b], so)
+            scale = 1.0 + np.abs(orc[b].x).max()
+            np.testing.assert_allclose(xs[b], orc[b].x, rtol=0, atol=1e-6 * scale)
+            np.testing.assert_allclose(us[b], orc[b].u, rtol=0, atol=1e-6 * (1 + np.abs(orc[b].u).max()))
+            np.testing.assert_allclose(u0[b], orc[b].u[0], rtol=0, atol=1e-6 * (1 + np.abs(orc[b].u).max()))
+            # tightening magnitudes: GPU stores icdf*sqrt(var) per stage variable
+            np.testing.assert_allclose(tight[b, :, :spec.nx], -sc[:spec.nx].T, rtol=1e-7, atol=1e-12)
+            np.testing.assert_allclose(tight[b, :H, spec.nx:], -ic[:spec.nu].T, rtol=1e-7, atol=1e-12)
+            prev[b] = (orc[b].x.T.copy(), orc[b].u.T.copy())
+        # next observation from the oracle's plant (same obs for both sides)
+        for b in range(B):
+            x0[b] = plant.rk4(x0[b], orc[b].u[0])[0]
+
+
+def test_status_codes_and_maxiter():
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem("quad2d", 50)
+    solver = BatchSolver(spec, 10, 2, max_iter=1)
+    solver.set_gps(product_gps(data, hyp))
+    solver.reset(reset_iterate=True)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, 2)
+    solver.solve(torch.tensor(x0, device="cuda"), torch.tensor(phase, dtype=torch.int32, device="cuda"))
+    st = solver.status.cpu().numpy()
+    it = solver.sqp_iter.cpu().numpy()
+    assert (st == 2).all() and (it == 1).all(), (st, it)
+
+
+def test_plant_step_matches_oracle():
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    for name in ("quad2d", "quad3d", "cartpole"):
+        spec, data, hyp = problem(name, 20)
+        solver = BatchSolver(spec, 5, 7)
+        rng = np.random.default_rng(3)
+        x = spec.reference_trajectory()[:, :7].T + 0.1 * rng.standard_normal((7, spec.nx))
+        u = spec.u_eq + 0.05 * rng.standard_normal((7, spec.nu))
+        ts = torch.zeros(7, dtype=torch.int32, device="cuda")
+        xn = solver.plant_step(torch.tensor(x, device="cuda"), torch.tensor(u, device="cuda"), ts).cpu().numpy()
+        dyn = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
+        for b in range(7):
+            np.testing.assert_allclose(xn[b], dyn.rk4(x[b], u[b])[0], rtol=1e-13, atol=1e-13)
+        assert (ts.cpu().numpy() == 1).all()
