@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""GP-MPC control steps/sec on MI355X (BASELINE.json metric, config 3 per GPU).
+
+Workload (per GPU, weak scaling): 2D quadrotor GP-MPC, N=200 GP training points, H=30,
+B=1024 independent MPC instances.  One "step" = one batched ``select_action`` over the B
+instances (variance kernel -> tightening + SQP-GN/IPM kernel) followed by the synthetic
+plant kernel that produces the next observation.  Inputs are resident in HBM; the GP,
+hyperparameters, initial states and reference are synthetic and seeded
+(gpmpc/synthetic.py).  N>1: one process per GPU (torch.distributed, RCCL), instances
+sharded by rank, no collective in the data path; barrier + max-over-ranks timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "GP-MPC control steps/sec, 2D quadrotor H=30 N=200, batch 1024 @1/2/4/8 GPU"
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 dense peak (vector and matrix are equal on gfx950)
+
+
+def gp_flops(spec, n_train, H):
+    """Algorithmic GP flops per instance.
+
+    mean+gradient: per linearisation, per stage, per evaluation, per training point:
+    2d (distance) + 2(d+1) (value + gradient contraction); state-dependent GPs are evaluated
+    at the 4 RK4 points, u-only GPs once per stage.  variance: triangular L^-1 k (N(N+1))
+    + squared norm (2N) per stage and GP.  exps counted separately.
+    """
+    per_lin = 0
+    exps_lin = 0
+    var = 0
+    for g, d in enumerate(spec.gp_dims):
+        state_dep = any(j < spec.nx for j in spec.gp_inputs[g])
+        evals = 4 if state_dep else 1
+        per_lin += H * evals * n_train * (4 * d + 2)
+        exps_lin += H * evals * n_train
+        var += H * (n_train * (n_train + 1) + 2 * n_train)
+    return per_lin, exps_lin, var
+
+
+def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats):
+    """Time the CPU oracle (numpy, 1 core) on a bounded closed-loop sample."""
+    from oracle import gpmpc_oracle as O
+    from gpmpc.synthetic import initial_states
+
+    sd = spec.to_dict()
+    gps = [O.ExactGP(X, y, *hyp[i]) for i, (X, y) in enumerate(data)]
+    sol = O.SQPSolver(sd, O.Dynamics(sd, gps), H)
+    plant = O.Dynamics(sd, None, params=spec.true_params)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, 1)
+    x = x0[0]
+    prev = None
+    times = []
+    t_start = time.perf_counter()
+    step = 0
+    while time.perf_counter() - t_start < seconds or step < 3:
+        t0 = time.perf_counter()
+        if prev is not None:
+            sc, ic = O.propagate_constraint_limits(sd, gps, prev[0], prev[1], *lqr_mats, 0.95)
+        else:
+            sc, ic = np.zeros((2 * spec.nx, H + 1)), np.zeros((2 * spec.nu, H))
+        lbx, ubx, lbu, ubu = O.stage_bounds(sd, sc, ic, -1e-8)
+        win = O.reference_window(traj, int(phase[0]) + step, H)
+        yref = np.zeros((H + 1, spec.nx + spec.nu))
+        yref[:, :spec.nx] = win.T
+        yref[:H, spec.nx:] = spec.u_eq
+        sol.solve(x, yref, lbx, ubx, lbu, ubu)
+        times.append(time.perf_counter() - t0)
+        prev = (sol.x.T.copy(), sol.u.T.copy())
+        x = plant.rk4(x, sol.u[0])[0]
+        step += 1
+    t = np.array(times[1:])  # drop the first step (gpmpc/plotting.py:25)
+    return {"value": float(1.0 / t.mean()), "unit": "control steps/s", "cores": 1, "kind": "port",
+            "sample": f"numpy oracle (dense-KKT IPM), 1 instance, {len(t)} closed-loop steps after the first, "
+                      f"{spec.name} N={data[0][0].shape[0]} H={H}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
+    ap.add_argument("--model", default="quad2d")
+    ap.add_argument("--n-train", type=int, default=200)
+    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from gpmpc import distributed as D
+    from gpmpc.gp import GaussianProcess
+    from gpmpc.models import get_spec
+    from gpmpc.solver import BatchSolver, setup_prior_dynamics
+    from gpmpc.synthetic import DEFAULT_HYPERS, initial_states, make_training_data
+
+    spec = get_spec(args.model)
+    H, B, N = args.horizon, args.batch, args.n_train
+    data = D.replicate_training_data(make_training_data(spec, N, seed=1), device=dev)  # GP replicated on every rank
+    hyp = DEFAULT_HYPERS[spec.name]
+    gps = []
+    for i, (X, y) in enumerate(data):
+        gp = GaussianProcess(torch.tensor(X), torch.tensor(y))
+        gp.set_hyperparameters(*hyp[i])
+        gps.append(gp)
+    Q, R = np.diag(spec.q_diag), np.diag(spec.r_diag)
+    dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
+    lqr_mats = setup_prior_dynamics(dfdx, dfdu, Q, R, spec.dt)
+
+    solver = BatchSolver(spec, H, B, device=dev)
+    solver.set_gps(gps)
+    solver.set_tightening(True, 0.95, *lqr_mats)
+    solver.reset(reset_iterate=True)
+    traj = spec.reference_trajectory()
+    # instances of this rank: global ids rank*B .. rank*B+B-1 (contiguous shards, no collective)
+    ids = D.shard_range(B, rank)
+    x0_all, phase_all = initial_states(spec, traj, B * world, seed=1)
+    obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
+    tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
+    acc_sqp = torch.zeros(B, dtype=torch.int64, device=dev)
+    acc_qp = torch.zeros(B, dtype=torch.int64, device=dev)
+    acc_st = torch.zeros(5, dtype=torch.int64, device=dev)
+    codes = torch.arange(5, device=dev, dtype=torch.int32)
+
+    def step():
+        u0 = solver.solve(obs, tstep)
+        solver.plant_step(obs, u0, tstep, out=obs)
+        acc_sqp.add_(solver.sqp_iter)
+        acc_qp.add_(solver.qp_iter)
+        acc_st.add_((solver.status[:, None] == codes[None, :]).sum(0))
+
+    solver.set_profiling(True)   # warm-up runs the timed body exactly (events, torch kernels)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    solver.kernel_times()  # drop warm-up events
+    for t in (acc_sqp, acc_qp, acc_st):
+        t.zero_()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t_enqueue = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    solver.set_profiling(False)
+    kt = solver.kernel_times()
+    stats = torch.tensor([elapsed, kt["sqp_ms"], kt["var_ms"]], dtype=torch.float64, device=dev)
+    sums = torch.stack([acc_sqp.sum(), acc_qp.sum()]).to(torch.float64)
+    status_counts = acc_st.to(torch.float64)
+    if dist is not None:
+        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
+    elapsed = float(stats[0])
+    total_instances = B * world
+    value = total_instances * args.steps / elapsed
+    sqp_mean = float(sums[0]) / (total_instances * args.steps)
+    qp_mean = float(sums[1]) / (total_instances * args.steps)
+
+    if rank == 0:
+        per_lin, exps_lin, var_flops = gp_flops(spec, N, H)
+        # dominant kernel: the SQP kernel; linearisations per instance-step = sqp_iter + 1
+        sqp_ms = float(stats[1]) / max(kt["sqp_launches"], 1)
+        flops_sqp = B * (sqp_mean + 1.0) * per_lin          # per launch (one rank's batch)
+        achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
+        var_ms = float(stats[2]) / max(kt["var_launches"], 1)
+        var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if kt["var_launches"] else None
+        cpu = None
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats)
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "control steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded GP training set, initial states, figure-eight reference)",
+            "config": {"workload": f"{spec.name} GP-MPC N={N} H={H}, {B} instances per GPU, closed loop",
+                       "model": spec.name, "global_batch": total_instances, "horizon": H, "n_train": N,
+                       "parallelism": f"instances sharded over {world} GPU(s), GP replicated"},
+            "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
+                         "traffic": None,
+                         "note": "FP64 GP mean+gradient contraction flops / HIP-event kernel time; peak = FP64 "
+                                 "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
+                                 "Riccati recursion"},
+            "roofline_variance": None if var_tf is None else {
+                "kernel": "gp_post_kernel<true>", "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},
+            "kernel_ms_per_step": {"sqp": sqp_ms, "variance": var_ms},
+            "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
+            "sqp_iter_mean": sqp_mean,
+            "qp_iter_mean_per_step": qp_mean,
+            "status_counts": {str(i): int(status_counts[i]) for i in range(5)},
+            "exps_per_sqp_launch": B * (sqp_mean + 1.0) * exps_lin,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

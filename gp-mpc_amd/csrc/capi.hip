@@ -70,13 +70,32 @@ struct gpmpc_handle {
     double* gp_vrows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
     double* gp_linvT[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
     int gp_npad[kMaxGP] = {0, 0, 0, 0};
+    // optional per-kernel HIP-event timing (bench.py's roofline leg)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_var, ev_sqp;
+    unsigned long long* timing = nullptr;  // diagnostic phase cycles (GPMPC_TIMING builds)
     int32_t* scratch_i = nullptr;   // [2][max_batch]
     double* scratch_d = nullptr;    // [max_batch][4]
 };
 
+static hipEvent_t take_event(gpmpc_handle* h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
 static void free_handle(gpmpc_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
+    for (auto* v : {&h->ev_var, &h->ev_sqp})
+        for (auto& pr : *v) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params})
         if (p) (void)hipFree(p);
     if (h->has_prev) (void)hipFree(h->has_prev);
@@ -360,7 +379,13 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     ProblemDev P = h->P;
     P.tighten = (h->P.tighten && h->P.use_gp) ? 1 : 0;
     // 1. GP variances at the previous solution (the MFMA contraction), only when needed
+    hipEvent_t e0 = nullptr, e1 = nullptr;
     if (P.tighten && h->any_prev) {
+        if (h->profiling) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (e0) HIPCHK(hipEventRecord(e0, s));
+        }
         for (int g = 0; g < h->md.ngp; ++g) {
             PostArgs a{};
             a.sx = h->x;
@@ -380,16 +405,65 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             a.var_off = g;
             HIPCHK(launch_gp_post(P.gp[g], h->gp_npad[g], a, true, s));
         }
+        if (e0 && e1) {
+            HIPCHK(hipEventRecord(e1, s));
+            h->ev_var.push_back({e0, e1});
+        }
     }
     // 2. the SQP step
     StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight};
-    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res};
+    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing};
     // optional outputs go to handle-owned scratch when NULL
     if (!io.sqp_iter) io.sqp_iter = h->scratch_i;
     if (!io.qp_iter) io.qp_iter = h->scratch_i + h->max_batch;
     if (!io.res) io.res = h->scratch_d;
+    e0 = e1 = nullptr;
+    if (h->profiling) {
+        e0 = take_event(h);
+        e1 = take_event(h);
+        if (e0) HIPCHK(hipEventRecord(e0, s));
+    }
     HIPCHK(launch_sqp(P, S, io, batch, s));
+    if (e0 && e1) {
+        HIPCHK(hipEventRecord(e1, s));
+        h->ev_sqp.push_back({e0, e1});
+    }
     h->any_prev = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    h->profiling = enabled != 0;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    (void)hipSetDevice(h->device);
+    auto sum = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
+        double acc = 0.0;
+        for (auto& pr : v) {
+            HIPCHK(hipEventSynchronize(pr.second));
+            float t = 0.0f;
+            HIPCHK(hipEventElapsedTime(&t, pr.first, pr.second));
+            acc += t;
+            h->ev_pool.push_back(pr.first);
+            h->ev_pool.push_back(pr.second);
+        }
+        if (ms) *ms = acc;
+        if (n) *n = (int32_t)v.size();
+        v.clear();
+        return GPMPC_OK;
+    };
+    gpmpc_status st = sum(h->ev_var, var_ms, n_var);
+    if (st != GPMPC_OK) return st;
+    return sum(h->ev_sqp, sqp_ms, n_sqp);
+}
+
+gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    h->timing = (unsigned long long*)timing_dev;
     return GPMPC_OK;
 }
 

@@ -76,6 +76,7 @@ struct StepIO {
     int32_t* sqp_iter;       // [B] out
     int32_t* qp_iter;        // [B] out, total IPM iterations
     double* res;             // [B][4] out, final NLP residuals (stat, eq, ineq, comp)
+    unsigned long long* timing;  // [B][8] phase cycles (GPMPC_TIMING builds only), may be null
 };
 
 // Arguments of the GP posterior kernel (gp_kernels.hip).

@@ -22,6 +22,21 @@ namespace gpmpc {
 
 #define WSYNC() __syncthreads()  // block == one wavefront: orders LDS traffic of the wave
 
+// Diagnostic phase timing (build with -DGPMPC_TIMING): shader-clock cycles per phase,
+// accumulated by the wave and stored per instance.  Phases: 0 tightening, 1 linearise,
+// 2 residuals/QP setup, 3 IPM vector work, 4 Riccati factor, 5 Riccati vector, 6 forward sweeps.
+#ifdef GPMPC_TIMING
+#define TPHASE(id)                                                   \
+    do {                                                             \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();  \
+        tacc[tcur] += t_ - tlast;                                    \
+        tlast = t_;                                                  \
+        tcur = (id);                                                 \
+    } while (0)
+#else
+#define TPHASE(id) do { } while (0)
+#endif
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -110,41 +125,43 @@ template <int ID>
 struct SqpKernel {
     using M = Model<ID>;
     static constexpr int NX = M::NX, NU = M::NU, NB = M::NB, NGP = M::NGP, NUNC = M::NUNC;
-    static constexpr int CB = 4;                       // tangent column block
+    static constexpr int GS = NB + 1;   // row stride of G'_k = [A_k | B_k | c_k]
+    static constexpr int PS = NX + 1;   // row stride of P'_k = [P_k | p_k] and K'_k = [K_k | kff_k]
+    static constexpr int CB = 4;        // tangent column block
     static constexpr int NCB = (NB + CB - 1) / CB;
+    // entries per Riccati phase and the rounds of 64 lanes they take
+    static constexpr int N1 = NX * GS;                       // W' = P' [G'; e]
+    static constexpr int N2 = GS * (GS + 1) / 2 - 1;         // upper triangle of M' (no corner)
+    static constexpr int N3P = NX * (NX + 1) / 2 + NX;       // P'_k (upper triangle + p column)
+    static constexpr int N3 = N3P + NU * PS;                 // + K'_k
+    static constexpr int R1 = (N1 + 63) / 64, R2 = (N2 + 63) / 64, R3 = (N3 + 63) / 64;
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *p, *K, *kff, *Rui, *hq, *gq, *cc, *dxv, *W, *Ms, *vs, *cd, *Sig;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig;
     };
     __host__ __device__ static size_t lds_doubles(int H) {
-        return (size_t)H * NX * NB          // G_k = [A_k B_k]
-               + (size_t)(H + 1) * NX * NX  // P_k
-               + (size_t)(H + 1) * NX       // p_k
-               + (size_t)H * NU * NX        // K_k
-               + (size_t)H * NU             // kff_k
-               + (size_t)H * NU * NU        // Ru_k^-1
-               + (size_t)(H + 1) * NB * 2   // hq, gq
-               + (size_t)H * NX             // cc
-               + (size_t)(H + 1) * NX       // dx
-               + (size_t)NX * NB + NB * NB + 2 * NB + NX  // W, M, vectors
-               + (size_t)H * NUNC           // cov_d diag per stage
+        return (size_t)H * NX * GS           // G'_k
+               + (size_t)(H + 1) * NX * PS   // P'_k
+               + (size_t)H * NU * PS         // K'_k
+               + (size_t)H * NU * NU         // Ru_k^-1
+               + (size_t)(H + 1) * NB * 2    // hq, gq
+               + (size_t)(H + 1) * NX        // dx (forward sweep)
+               + (size_t)NX * GS + GS * GS + 2 * NB + NX  // W', M', vectors
+               + (size_t)H * NUNC            // cov_d diag per stage
                + (size_t)2 * NX * NX + NU * NX;  // Sigma, T scratch
     }
     __device__ static Lds carve(double* s, int H) {
         Lds L;
-        L.G = s;   s += (size_t)H * NX * NB;
-        L.P = s;   s += (size_t)(H + 1) * NX * NX;
-        L.p = s;   s += (size_t)(H + 1) * NX;
-        L.K = s;   s += (size_t)H * NU * NX;
-        L.kff = s; s += (size_t)H * NU;
+        L.G = s;   s += (size_t)H * NX * GS;
+        L.P = s;   s += (size_t)(H + 1) * NX * PS;
+        L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
         L.hq = s;  s += (size_t)(H + 1) * NB;
         L.gq = s;  s += (size_t)(H + 1) * NB;
-        L.cc = s;  s += (size_t)H * NX;
         L.dxv = s; s += (size_t)(H + 1) * NX;
-        L.W = s;   s += (size_t)NX * NB;
-        L.Ms = s;  s += (size_t)NB * NB;
+        L.W = s;   s += (size_t)NX * GS;
+        L.Ms = s;  s += (size_t)GS * GS;
         L.vs = s;  s += (size_t)2 * NB + NX;
         L.cd = s;  s += (size_t)H * NUNC;
         L.Sig = s;
@@ -208,7 +225,8 @@ struct SqpKernel {
 
     // ------------------------------------------------------------------ linearisation
     // Every lane computes RK4 for stage s = lane % H (its chunk of the GP sums); chunk-c lanes
-    // then build tangent column blocks jb with jb % C == c.  Lane s (chunk 0) returns F_s.
+    // then build tangent column blocks jb with jb % C == c.  Lane s (chunk 0) returns F_s and
+    // G'_s[:, 0:NB] = [A_s B_s] lands in LDS.
     __device__ static void linearize(const ProblemDev& P, const Lds& L, int H, int lane, const double (&w)[NB],
                                      double (&F)[NX]) {
         const int C = max(1, 64 / H);
@@ -265,191 +283,270 @@ struct SqpKernel {
                     }
             }
             if (chunk < C) {
-                double* Gs = L.G + (size_t)stage * NX * NB;
+                double* Gs = L.G + (size_t)stage * NX * GS;
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
 #pragma unroll
                     for (int j = 0; j < CB; ++j)
-                        if (j0 + j < NB) Gs[i * NB + j0 + j] = dF[i][j];
+                        if (j0 + j < NB) Gs[i * GS + j0 + j] = dF[i][j];
             }
         }
     }
 
-
     // ------------------------------------------------------------------ Riccati recursion
-    // Newton system of the IPM: min sum_k 1/2 w_k' diag(hq_k) w_k + gq_k' w_k
-    //   s.t. dx_{k+1} = A_k dx_k + B_k du_k + cc_k, dx_0 = 0.
-    // Backward sweep (factorisation + vector); stores K_k, kff_k, Ru_k^-1, P_k, p_k.
-    __device__ static bool riccati_factor(const Lds& L, int H, int lane) {
-        // P_H = diag(hq_H[x]), p_H = gq_H[x]
-        double* PH = L.P + (size_t)H * NX * NX;
-        for (int e = lane; e < NX * NX; e += 64) PH[e] = (e / NX == e % NX) ? L.hq[H * NB + e / NX] : 0.0;
-        if (lane < NX) L.p[H * NX + lane] = L.gq[H * NB + lane];
+    // Newton system of the IPM (HPIPM's backward/forward Riccati structure):
+    //   min sum_k 1/2 w_k' diag(hq_k) w_k + gq_k' w_k   s.t.  dx_{k+1} = A_k dx_k + B_k du_k + c_k, dx_0 = 0
+    // with w_k = [dx_k; du_k], G'_k = [A_k B_k c_k].  Sequential over stages, parallel over the
+    // entries of each stage's small dense products (one lane per entry, uniform code paths).
+    struct Entries {   // per-lane (row, col) of each phase, decoded once per sweep
+        int8_t i1[R1], j1[R1], i2[R2], j2[R2], i3[R3], j3[R3];
+    };
+    __device__ static Entries decode(int lane) {
+        Entries E;
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int e = lane + 64 * r;
+            E.i1[r] = e < N1 ? e / GS : -1;
+            E.j1[r] = e < N1 ? e % GS : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {  // upper triangle of GS x GS, row-major, minus (NB, NB)
+            int e = lane + 64 * r, i = -1, j = 0;
+            if (e < N2) {
+                i = 0;
+                while (e >= GS - i) { e -= GS - i; ++i; }
+                j = i + e;
+            }
+            E.i2[r] = i;
+            E.j2[r] = j;
+        }
+#pragma unroll
+        for (int r = 0; r < R3; ++r) {  // P' entries (i <= j, j in [0,NX) or j = NB), then K' entries (a, j)
+            int e = lane + 64 * r, i = -1, j = 0;
+            if (e < N3P) {
+                i = 0;
+                while (e >= NX + 1 - i) { e -= NX + 1 - i; ++i; }
+                j = i + e;
+                if (j == NX) j = NB;   // p column
+            } else if (e < N3) {
+                e -= N3P;
+                i = NX + e / PS;       // i >= NX marks a K' entry of input row a = i - NX
+                j = e % PS;
+                if (j == NX) j = NB;
+            }
+            E.i3[r] = i;
+            E.j3[r] = j;
+        }
+        return E;
+    }
+
+    // Phase 1: W'[l][j] = sum_m P'[l][m] G'[m][j] (+ p_l for the c column).
+    __device__ static void phase_W(const Lds& L, const double* Pn, const double* G, const Entries& E) {
+#pragma unroll
+        for (int r = 0; r < R1; ++r) {
+            const int l = E.i1[r], j = E.j1[r];
+            if (l >= 0) {
+                double pr[PS], gc[NX];
+#pragma unroll
+                for (int m = 0; m < PS; ++m) pr[m] = Pn[l * PS + m];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) gc[m] = G[m * GS + j];
+                double acc = (j == NB) ? pr[NX] : 0.0;
+#pragma unroll
+                for (int m = 0; m < NX; ++m) acc = fma(pr[m], gc[m], acc);
+                L.W[l * GS + j] = acc;
+            }
+        }
+    }
+
+    // Phase 2: M'[i][j] = diag(hq) / gq + sum_l G'[l][i] W'[l][j], upper triangle.
+    __device__ static void phase_M(const Lds& L, const double* G, const double* hq, const double* gq, const Entries& E) {
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+            const int i = E.i2[r], j = E.j2[r];
+            if (i >= 0) {
+                double gi[NX], wj[NX];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) { gi[l] = G[l * GS + i]; wj[l] = L.W[l * GS + j]; }
+                double acc = (i == j) ? hq[i] : ((j == NB) ? gq[i] : 0.0);
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(gi[l], wj[l], acc);
+                L.Ms[i * GS + j] = acc;
+            }
+        }
+    }
+
+    __device__ static bool load_Ri(const Lds& L, double (&Ri)[NU][NU]) {
+        double Ru[NU][NU];
+#pragma unroll
+        for (int a = 0; a < NU; ++a)
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2)
+                Ru[a][b2] = L.Ms[(NX + min(a, b2)) * GS + NX + max(a, b2)];
+        return spd_inverse<NU>(Ru, Ri);
+    }
+
+    // M'[NX+b][j] for j in [0,NX) (lower triangle -> read the mirror) or j = NB.
+    __device__ static double mcol(const Lds& L, int b2, int j) {
+        return j < NX ? L.Ms[j * GS + NX + b2] : L.Ms[(NX + b2) * GS + NB];
+    }
+
+    __device__ static bool riccati_factor(const Lds& L, int H, int lane, const Entries& E) {
+        // P'_H = [diag(hq_H[x]) | gq_H[x]]
+        double* PH = L.P + (size_t)H * NX * PS;
+        for (int e = lane; e < NX * PS; e += 64) {
+            const int i = e / PS, j = e % PS;
+            PH[e] = (j == NX) ? L.gq[H * NB + i] : ((i == j) ? L.hq[H * NB + i] : 0.0);
+        }
         WSYNC();
         bool ok = true;
         for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * NX * NX;
-            const double* pn = L.p + (size_t)(k + 1) * NX;
-            const double* G = L.G + (size_t)k * NX * NB;
-            const double* c = L.cc + (size_t)k * NX;
-            double* pv = L.vs;            // NX
-            double* gv = L.vs + NX;       // NB
-            // phase 1: W = P_{k+1} G_k, pv = P_{k+1} c_k + p_{k+1}
-            for (int e = lane; e < NX * NB + NX; e += 64) {
-                if (e < NX * NB) {
-                    const int l = e / NB, j = e % NB;
-                    double acc = 0.0;
-#pragma unroll
-                    for (int m = 0; m < NX; ++m) acc = fma(Pn[l * NX + m], G[m * NB + j], acc);
-                    L.W[e] = acc;
-                } else {
-                    const int i = e - NX * NB;
-                    double acc = pn[i];
-#pragma unroll
-                    for (int m = 0; m < NX; ++m) acc = fma(Pn[i * NX + m], c[m], acc);
-                    pv[i] = acc;
-                }
-            }
+            const double* Pn = L.P + (size_t)(k + 1) * NX * PS;
+            const double* G = L.G + (size_t)k * NX * GS;
+            phase_W(L, Pn, G, E);
             WSYNC();
-            // phase 2: M = diag(hq_k) + G' W, gv = gq_k + G' pv
-            for (int e = lane; e < NB * NB + NB; e += 64) {
-                if (e < NB * NB) {
-                    const int i = e / NB, j = e % NB;
-                    double acc = (i == j) ? L.hq[k * NB + i] : 0.0;
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + i], L.W[l * NB + j], acc);
-                    L.Ms[e] = acc;
-                } else {
-                    const int j = e - NB * NB;
-                    double acc = L.gq[k * NB + j];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + j], pv[l], acc);
-                    gv[j] = acc;
-                }
-            }
+            phase_M(L, G, L.hq + k * NB, L.gq + k * NB, E);
             WSYNC();
-            // phase 3: Schur complement onto the state block
-            double Ru[NU][NU], Ri[NU][NU];
+            double Ri[NU][NU];
+            ok = load_Ri(L, Ri) && ok;
+            double* Pk = L.P + (size_t)k * NX * PS;
+            double* Kk = L.K + (size_t)k * NU * PS;
 #pragma unroll
-            for (int a = 0; a < NU; ++a)
+            for (int r = 0; r < R3; ++r) {
+                const int i = E.i3[r], j = E.j3[r];
+                if (i < 0 || (i < NX && k == 0)) continue;   // P_0 is not needed
+                double mj[NU], tr[NU];
 #pragma unroll
-                for (int b2 = 0; b2 < NU; ++b2) Ru[a][b2] = L.Ms[(NX + a) * NB + NX + b2];
-            ok = spd_inverse<NU>(Ru, Ri) && ok;
-            const int nP = (k >= 1) ? NX * NX : 0;
-            for (int e = lane; e < nP + NX + NU * NX + NU + NU * NU; e += 64) {
-                if (e < nP) {
-                    const int i = e / NX, j = e % NX;
-                    double acc = L.Ms[i * NB + j];
+                for (int b2 = 0; b2 < NU; ++b2) mj[b2] = mcol(L, b2, j);
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) {
-                        double t = 0.0;
-#pragma unroll
-                        for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], L.Ms[(NX + b2) * NB + j], t);
-                        acc = fma(-L.Ms[(NX + a) * NB + i], t, acc);
-                    }
-                    L.P[(size_t)k * NX * NX + e] = acc;
-                } else if (e < nP + NX) {
-                    const int i = e - nP;
-                    double acc = gv[i];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) {
-                        double t = 0.0;
-#pragma unroll
-                        for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], gv[NX + b2], t);
-                        acc = fma(-L.Ms[(NX + a) * NB + i], t, acc);
-                    }
-                    L.p[(size_t)k * NX + i] = acc;
-                } else if (e < nP + NX + NU * NX) {
-                    const int q = e - nP - NX, a = q / NX, i = q % NX;
+                for (int a = 0; a < NU; ++a) {   // tr = Ru^-1 M'[u, j]  (no runtime-indexed arrays)
                     double t = 0.0;
 #pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], L.Ms[(NX + b2) * NB + i], t);
-                    L.K[(size_t)k * NU * NX + q] = -t;
-                } else if (e < nP + NX + NU * NX + NU) {
-                    const int a = e - nP - NX - NU * NX;
+                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], mj[b2], t);
+                    tr[a] = t;
+                }
+                const int jj = (j == NB) ? NX : j;
+                if (i < NX) {
+                    double mi[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) mi[a] = L.Ms[i * GS + NX + a];
+                    double acc = L.Ms[i * GS + j];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc = fma(-mi[a], tr[a], acc);
+                    Pk[i * PS + jj] = acc;
+                    if (j < NX && j != i) Pk[j * PS + i] = acc;
+                } else {
                     double t = 0.0;
 #pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], gv[NX + b2], t);
-                    L.kff[k * NU + a] = -t;
-                } else {
-                    const int q = e - nP - NX - NU * NX - NU;
-                    L.Rui[(size_t)k * NU * NU + q] = Ri[q / NU][q % NU];
+                    for (int a = 0; a < NU; ++a) t = (i - NX == a) ? tr[a] : t;
+                    Kk[(i - NX) * PS + jj] = -t;
                 }
+            }
+            if (lane < NU * NU) {
+                double rv = 0.0;
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
+                L.Rui[(size_t)k * NU * NU + lane] = rv;
             }
             WSYNC();
         }
         return ok;
     }
 
-    // Vector-only backward sweep with the stored factorisation (Mehrotra corrector).
+    // Vector-only backward sweep with the stored factorisation (Mehrotra corrector): p, kff.
     __device__ static void riccati_vector(const Lds& L, int H, int lane) {
-        if (lane < NX) L.p[H * NX + lane] = L.gq[H * NB + lane];
+        if (lane < NX) L.P[(size_t)H * NX * PS + lane * PS + NX] = L.gq[H * NB + lane];
         WSYNC();
         for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * NX * NX;
-            const double* pn = L.p + (size_t)(k + 1) * NX;
-            const double* G = L.G + (size_t)k * NX * NB;
-            const double* c = L.cc + (size_t)k * NX;
+            const double* Pn = L.P + (size_t)(k + 1) * NX * PS;
+            const double* G = L.G + (size_t)k * NX * GS;
             double* pv = L.vs;
             if (lane < NX) {
-                double acc = pn[lane];
+                double pr[PS], c[NX];
 #pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(Pn[lane * NX + m], c[m], acc);
+                for (int m = 0; m < PS; ++m) pr[m] = Pn[lane * PS + m];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) c[m] = G[m * GS + NB];
+                double acc = pr[NX];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) acc = fma(pr[m], c[m], acc);
                 pv[lane] = acc;
             }
             WSYNC();
             // gv_j = gq_kj + sum_l G_lj pv_l ; p_k = gv_x + K' gv_u ; kff = -Ru^-1 gv_u
             if (lane < NX + NU) {
+                double pvl[NX];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) pvl[l] = pv[l];
                 double gu[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
+                    double gcol[NX];
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) gcol[l] = G[l * GS + NX + a];
                     double acc = L.gq[k * NB + NX + a];
 #pragma unroll
-                    for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + NX + a], pv[l], acc);
+                    for (int l = 0; l < NX; ++l) acc = fma(gcol[l], pvl[l], acc);
                     gu[a] = acc;
                 }
                 if (lane < NX) {
                     if (k >= 1) {
                         const int i = lane;
+                        double gcol[NX], kc[NU];
+#pragma unroll
+                        for (int l = 0; l < NX; ++l) gcol[l] = G[l * GS + i];
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) kc[a] = L.K[(size_t)k * NU * PS + a * PS + i];
                         double acc = L.gq[k * NB + i];
 #pragma unroll
-                        for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + i], pv[l], acc);
+                        for (int l = 0; l < NX; ++l) acc = fma(gcol[l], pvl[l], acc);
 #pragma unroll
-                        for (int a = 0; a < NU; ++a) acc = fma(L.K[(size_t)k * NU * NX + a * NX + i], gu[a], acc);
-                        L.p[(size_t)k * NX + i] = acc;
+                        for (int a = 0; a < NU; ++a) acc = fma(kc[a], gu[a], acc);
+                        L.P[(size_t)k * NX * PS + i * PS + NX] = acc;
                     }
                 } else {
                     const int a = lane - NX;
+                    double ri[NU];
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) ri[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
                     double t = 0.0;
 #pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) t = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], gu[b2], t);
-                    L.kff[k * NU + a] = -t;
+                    for (int b2 = 0; b2 < NU; ++b2) t = fma(ri[b2], gu[b2], t);
+                    L.K[(size_t)k * NU * PS + a * PS + NX] = -t;
                 }
             }
             WSYNC();
         }
     }
 
-    // Forward sweep: dx_0 = 0, du_k = K_k dx_k + kff_k, dx_{k+1} = A dx_k + B du_k + cc_k.
+    // Forward sweep: dx_0 = 0, du_k = K'_k [dx_k; 1], dx_{k+1} = G'_k [dx_k; du_k; 1].
     __device__ static void riccati_forward(const Lds& L, int H, int lane) {
         if (lane < NX) L.dxv[lane] = 0.0;
         WSYNC();
         for (int k = 0; k < H; ++k) {
             if (lane < NX) {
-                const double* dx = L.dxv + (size_t)k * NX;
-                const double* G = L.G + (size_t)k * NX * NB;
-                double xk[NX];
+                const double* G = L.G + (size_t)k * NX * GS;
+                const double* Kk = L.K + (size_t)k * NU * PS;
+                double xk[NX], kr[NU][PS], gr[GS];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) xk[j] = dx[j];
-                double acc = L.cc[k * NX + lane];
+                for (int j = 0; j < NX; ++j) xk[j] = L.dxv[(size_t)k * NX + j];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) acc = fma(G[lane * NB + j], xk[j], acc);
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j < PS; ++j) kr[a][j] = Kk[a * PS + j];
+#pragma unroll
+                for (int j = 0; j < GS; ++j) gr[j] = G[lane * GS + j];
+                double acc = gr[NB];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) acc = fma(gr[j], xk[j], acc);
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    double du = L.kff[k * NU + a];
+                    double du = kr[a][NX];
 #pragma unroll
-                    for (int j = 0; j < NX; ++j) du = fma(L.K[(size_t)k * NU * NX + a * NX + j], xk[j], du);
-                    acc = fma(G[lane * NB + NX + a], du, acc);
+                    for (int j = 0; j < NX; ++j) du = fma(kr[a][j], xk[j], du);
+                    acc = fma(gr[NX + a], du, acc);
                 }
                 L.dxv[(size_t)(k + 1) * NX + lane] = acc;
             }
@@ -457,34 +554,38 @@ struct SqpKernel {
         }
     }
 
-    // Per-lane step from the Riccati solution: dd (stage k variables) and dpi_k.
+    // Per-lane step of stage k from the Riccati solution: dd = [dx_k; du_k] and dpi_k.
     __device__ static void recover_step(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
         const bool on = lane <= H;
-        double dx[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dx[i] = (on && lane >= 1) ? L.dxv[(size_t)lane * NX + i] : 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dd[i] = dx[i];
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            double du = 0.0;
-            if (lane < H) {
-                du = L.kff[lane * NU + a];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) du = fma(L.K[(size_t)lane * NU * NX + a * NX + j], dx[j], du);
-            }
-            dd[NX + a] = du;
-        }
+        double dx[NX], dxn[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double acc = 0.0;
-            if (lane < H) {
-                acc = L.p[(size_t)(lane + 1) * NX + i];
+            dx[i] = (on && lane >= 1) ? L.dxv[(size_t)lane * NX + i] : 0.0;
+            dxn[i] = (lane < H) ? L.dxv[(size_t)(lane + 1) * NX + i] : 0.0;
+        }
 #pragma unroll
-                for (int j = 0; j < NX; ++j)
-                    acc = fma(L.P[(size_t)(lane + 1) * NX * NX + i * NX + j], L.dxv[(size_t)(lane + 1) * NX + j], acc);
-            }
-            dpi[i] = -acc;
+        for (int i = 0; i < NX; ++i) dd[i] = dx[i];
+        const int kk = min(lane, H - 1);
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double kr[PS];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) kr[j] = L.K[(size_t)kk * NU * PS + a * PS + j];
+            double du = kr[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) du = fma(kr[j], dx[j], du);
+            dd[NX + a] = (lane < H) ? du : 0.0;
+        }
+        const double* Pn = L.P + (size_t)(kk + 1) * NX * PS;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double pr[PS];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) pr[j] = Pn[i * PS + j];
+            double acc = pr[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(pr[j], dxn[j], acc);
+            dpi[i] = (lane < H) ? -acc : 0.0;
         }
     }
 
@@ -493,15 +594,18 @@ struct SqpKernel {
         double pim1[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) pim1[i] = __shfl(pi[i], lane > 0 ? lane - 1 : 0);
-        const double* G = L.G + (size_t)min(lane, H - 1) * NX * NB;
+        const double* G = L.G + (size_t)min(lane, H - 1) * NX * GS;
+        double g[NX][NB];
+#pragma unroll
+        for (int l = 0; l < NX; ++l)
+#pragma unroll
+            for (int j = 0; j < NB; ++j) g[l][j] = G[l * GS + j];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             double acc = 0.0;
-            if (lane < H) {
 #pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(G[l * NB + j], pi[l], acc);
-            }
-            out[j] = -acc + ((j < NX && lane >= 1 && lane <= H) ? pim1[j] : 0.0);
+            for (int l = 0; l < NX; ++l) acc = fma(g[l][j], pi[l], acc);
+            out[j] = ((lane < H) ? -acc : 0.0) + ((j < NX && lane >= 1 && lane <= H) ? pim1[j] : 0.0);
         }
     }
 
@@ -511,20 +615,26 @@ struct SqpKernel {
         double xn[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) xn[i] = __shfl(d[i], lane < 63 ? lane + 1 : 63);
-        const double* G = L.G + (size_t)min(lane, H - 1) * NX * NB;
+        const double* G = L.G + (size_t)min(lane, H - 1) * NX * GS;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double acc = 0.0;
-            if (lane < H) {
-                acc = xn[i] - c[i];
+            double gr[NB];
 #pragma unroll
-                for (int j = 0; j < NB; ++j) acc = fma(-G[i * NB + j], d[j], acc);
-            }
-            r[i] = acc;
+            for (int j = 0; j < NB; ++j) gr[j] = G[i * GS + j];
+            double acc = xn[i] - c[i];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc = fma(-gr[j], d[j], acc);
+            r[i] = (lane < H) ? acc : 0.0;
         }
     }
 
     __device__ static double max_step(double v, double dv) { return dv < 0.0 ? -v / dv : 1e300; }
+
+    // cost Hessian diagonal of stage variable v on lane k (acados cost_scaling: dt on stages, 1 terminal)
+    __device__ static double hdiag(const ProblemDev& P, int v, int lane, int H) {
+        if (v < NX) return (lane >= 1 && lane <= H) ? ((lane < H) ? P.cost_scale : 1.0) * P.q[v] : 1.0;
+        return (lane < H) ? P.cost_scale * P.r[v - NX] : 1.0;
+    }
 
     // ------------------------------------------------------------------ the kernel body
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
@@ -537,7 +647,11 @@ struct SqpKernel {
         const bool act_x = on && lane >= 1;
         const bool act_u = lane < H;
         const int k = min(lane, H);
-
+#ifdef GPMPC_TIMING
+        unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long tlast = __builtin_amdgcn_s_memtime();
+        int tcur = 7;
+#endif
         // ---------------- load instance state (acados memory: iterate + multipliers)
         double w[NB], lamL[NB], lamU[NB], pi[NX];
         const double* xg = S.x + (size_t)b * (H + 1) * NX;
@@ -557,23 +671,9 @@ struct SqpKernel {
         double x0[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) x0[i] = io.x0[(size_t)b * NX + i];
+        const int tref = (io.tstep[b] + k) % P.traj_len;
 
-        // ---------------- reference window and cost (gpmpc.py:356-361, 231-239)
-        double yr[NB], hd[NB];
-        {
-            const int t = (io.tstep[b] + k) % P.traj_len;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                yr[i] = P.traj[(size_t)t * NX + i];
-                hd[i] = act_x ? (lane < H ? P.cost_scale : 1.0) * P.q[i] : 1.0;
-            }
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                yr[NX + a] = P.u_eq[a];
-                hd[NX + a] = act_u ? P.cost_scale * P.r[a] : 1.0;
-            }
-        }
-
+        TPHASE(0);
         // ---------------- constraint tightening from the previous solution (gpmpc.py:425-498)
         double tsd[NB];  // icdf * sqrt(variance) per stage variable
 #pragma unroll
@@ -600,19 +700,14 @@ struct SqpKernel {
             for (int kk = 0; kk <= H; ++kk) {
                 // record sqrt(diag Sigma_k) and sqrt(diag K Sigma_k K')
                 for (int e = lane; e < NX * NX + NU * NX; e += 64) {
-                    if (e < NX * NX) {
-                        const int i = e / NX, j = e % NX;
-                        double acc = 0.0;
+                    const bool isT = e < NX * NX;
+                    const int q = isT ? e : e - NX * NX;
+                    const int i = q / NX, j = q % NX;
+                    const double* rowA = isT ? P.Acl + i * NX : P.K + i * NX;
+                    double acc = 0.0;
 #pragma unroll
-                        for (int m = 0; m < NX; ++m) acc = fma(P.Acl[i * NX + m], Sig[m * NX + j], acc);
-                        T1[e] = acc;
-                    } else {
-                        const int q = e - NX * NX, a = q / NX, j = q % NX;
-                        double acc = 0.0;
-#pragma unroll
-                        for (int m = 0; m < NX; ++m) acc = fma(P.K[a * NX + m], Sig[m * NX + j], acc);
-                        U[q] = acc;
-                    }
+                    for (int m = 0; m < NX; ++m) acc = fma(rowA[m], Sig[m * NX + j], acc);
+                    (isT ? T1 : U)[q] = acc;
                 }
                 if (lane < NX) L.hq[kk * NB + lane] = P.icdf * sqrt(fmax(Sig[lane * NX + lane], 0.0));
                 WSYNC();
@@ -646,26 +741,26 @@ struct SqpKernel {
             for (int v = 0; v < NB; ++v) S.tight[((size_t)b * (H + 1) + k) * NB + v] = tsd[v];
         }
         // tightened boxes lo + t - uh <= w <= hi - t + uh   (gpmpc.py:296-314)
-        double lb[NB], ub[NB];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            lb[i] = P.x_lo[i] + tsd[i] - P.uh;
-            ub[i] = P.x_hi[i] - tsd[i] + P.uh;
-        }
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            lb[NX + a] = P.u_lo[a] + tsd[NX + a] - P.uh;
-            ub[NX + a] = P.u_hi[a] - tsd[NX + a] + P.uh;
-        }
+        auto lbv = [&](int v) { return (v < NX ? P.x_lo[v] : P.u_lo[v - NX]) + tsd[v] - P.uh; };
+        auto ubv = [&](int v) { return (v < NX ? P.x_hi[v] : P.u_hi[v - NX]) - tsd[v] + P.uh; };
 
+        const Entries E = decode(lane);
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
         const double nc = 2.0 * (double)H * (double)NB;
         int status = kMaxIter, it = 0, qp_total = 0;
         double res[4] = {0, 0, 0, 0};
         for (it = 0;; ++it) {
             double F[NX];
+            TPHASE(1);
             linearize(P, L, H, lane, w, F);
             WSYNC();
+            TPHASE(2);
+            // stage reference (gpmpc.py:356-361)
+            double yr[NB];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) yr[i] = P.traj[(size_t)tref * NX + i];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) yr[NX + a] = P.u_eq[a];
             // NLP residuals with the current multipliers
             double ct[NB];
             ctpi(L, H, lane, pi, ct);
@@ -673,13 +768,16 @@ struct SqpKernel {
 #pragma unroll
             for (int i = 0; i < NX; ++i) xn[i] = __shfl(w[i], lane < 63 ? lane + 1 : 63);
             double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0;
+            double g[NB];
 #pragma unroll
             for (int v = 0; v < NB; ++v) {
                 const bool av = v < NX ? act_x : act_u;
+                g[v] = av ? hdiag(P, v, lane, H) * (w[v] - yr[v]) : 0.0;
                 if (av) {
-                    r_stat = fmax(r_stat, fabs(hd[v] * (w[v] - yr[v]) - lamL[v] + lamU[v] + ct[v]));
-                    r_ineq = fmax(r_ineq, fmax(lb[v] - w[v], w[v] - ub[v]));
-                    r_comp = fmax(r_comp, fmax(fabs(lamL[v] * (w[v] - lb[v])), fabs(lamU[v] * (ub[v] - w[v]))));
+                    const double lb = lbv(v), ub = ubv(v);
+                    r_stat = fmax(r_stat, fabs(g[v] - lamL[v] + lamU[v] + ct[v]));
+                    r_ineq = fmax(r_ineq, fmax(lb - w[v], w[v] - ub));
+                    r_comp = fmax(r_comp, fmax(fabs(lamL[v] * (w[v] - lb)), fabs(lamU[v] * (ub - w[v]))));
                 }
             }
             double cq[NX];
@@ -704,142 +802,157 @@ struct SqpKernel {
             if (it == P.max_iter) { status = kMaxIter; break; }
 
             // ---------------- QP in the step variables (HPIPM's role), Mehrotra IPM
-            double lbd[NB], ubd[NB], g[NB], d[NB], sl[NB], su[NB], ll[NB], lu[NB], piq[NX];
+            double d[NB], sl[NB], su[NB], ll[NB], lu[NB], piq[NX];
 #pragma unroll
             for (int v = 0; v < NB; ++v) {
                 const bool av = v < NX ? act_x : act_u;
-                g[v] = av ? hd[v] * (w[v] - yr[v]) : 0.0;
-                lbd[v] = lb[v] - w[v];
-                ubd[v] = ub[v] - w[v];
                 d[v] = (lane == 0 && v < NX) ? x0[v] - w[v] : 0.0;   // dx_0 = e0 fixed
-                sl[v] = av ? fmax(-lbd[v], 1e-2) : 1.0;
-                su[v] = av ? fmax(ubd[v], 1e-2) : 1.0;
+                sl[v] = av ? fmax(w[v] - lbv(v), 1e-2) : 1.0;
+                su[v] = av ? fmax(ubv(v) - w[v], 1e-2) : 1.0;
                 ll[v] = av ? P.qp_mu0 / sl[v] : 0.0;
                 lu[v] = av ? P.qp_mu0 / su[v] : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) piq[i] = 0.0;
-            if (act_u) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) L.cc[lane * NX + i] = 0.0;  // placeholder, set per IPM iteration
-            }
             bool qp_ok = true;
             int qit = 0;
+            TPHASE(3);
             for (qit = 0; qit < P.qp_max_iter; ++qit) {
-                double rd[NB], rl[NB], ru[NB], rp[NX], ctq[NB];
-                ctpi(L, H, lane, piq, ctq);
-                dyn_residual(L, H, lane, d, cq, rp);
-                double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
+                double rp[NX];
+                {
+                    double ctq[NB];
+                    ctpi(L, H, lane, piq, ctq);
+                    dyn_residual(L, H, lane, d, cq, rp);
+                    double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
 #pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    rd[v] = av ? fma(hd[v], d[v], g[v]) - ll[v] + lu[v] + ctq[v] : 0.0;
-                    rl[v] = av ? d[v] - lbd[v] - sl[v] : 0.0;
-                    ru[v] = av ? ubd[v] - d[v] - su[v] : 0.0;
-                    m_rd = fmax(m_rd, fabs(rd[v]));
-                    m_lu = fmax(m_lu, fmax(fabs(rl[v]), fabs(ru[v])));
-                    mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
-                }
-#pragma unroll
-                for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
-                const double mu = wave_sum(mu_l) / nc;
-                m_rd = wave_max(m_rd);
-                m_rb = wave_max(m_rb);
-                m_lu = wave_max(m_lu);
-                if (!(mu == mu) || !(m_rd == m_rd)) { qp_ok = false; break; }
-                if (m_rd <= P.qp_tol && m_rb <= P.qp_tol && m_lu <= P.qp_tol && mu <= P.qp_tol) break;
-
-                // Riccati data: hq = H + Sigma, cc = -r_pi ; gq for the predictor
-                double sig[NB];
-#pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    sig[v] = av ? ll[v] / sl[v] + lu[v] / su[v] : 0.0;
-                    if (on) {
-                        L.hq[k * NB + v] = hd[v] + sig[v];
-                        // predictor: r_ml = ll sl, r_mu = lu su
-                        L.gq[k * NB + v] = av ? rd[v] + (ll[v] * sl[v] + ll[v] * rl[v]) / sl[v]
-                                                      - (lu[v] * su[v] + lu[v] * ru[v]) / su[v] : 0.0;
+                    for (int v = 0; v < NB; ++v) {
+                        const bool av = v < NX ? act_x : act_u;
+                        const double rd = av ? fma(hdiag(P, v, lane, H), d[v], g[v]) - ll[v] + lu[v] + ctq[v] : 0.0;
+                        const double rl = av ? d[v] - (lbv(v) - w[v]) - sl[v] : 0.0;
+                        const double ru = av ? (ubv(v) - w[v]) - d[v] - su[v] : 0.0;
+                        m_rd = fmax(m_rd, fabs(rd));
+                        m_lu = fmax(m_lu, fmax(fabs(rl), fabs(ru)));
+                        mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
+                        if (on) {
+                            // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
+                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] / sl[v] + lu[v] / su[v] : 0.0);
+                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl / sl[v] - lu[v] - lu[v] * ru / su[v] : 0.0;
+                        }
                     }
-                }
-                if (act_u) {
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) L.cc[lane * NX + i] = -rp[i];
-                }
-                WSYNC();
-                if (!riccati_factor(L, H, lane)) { qp_ok = false; break; }
-                riccati_forward(L, H, lane);
-                double dd[NB], dp[NX], dsl[NB], dsu[NB], dll[NB], dlu[NB];
-                recover_step(L, H, lane, dd, dp);
-                double amax = 1.0;
+                    for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
+                    const double mu = wave_sum(mu_l) / nc;
+                    m_rd = wave_max(m_rd);
+                    m_rb = wave_max(m_rb);
+                    m_lu = wave_max(m_lu);
+                    if (!(mu == mu) || !(m_rd == m_rd)) { qp_ok = false; break; }
+                    if (m_rd <= P.qp_tol && m_rb <= P.qp_tol && m_lu <= P.qp_tol && mu <= P.qp_tol) break;
+                    if (act_u) {
 #pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    dsl[v] = av ? dd[v] + rl[v] : 0.0;
-                    dsu[v] = av ? -dd[v] + ru[v] : 0.0;
-                    dll[v] = av ? (-ll[v] * sl[v] - ll[v] * dsl[v]) / sl[v] : 0.0;
-                    dlu[v] = av ? (-lu[v] * su[v] - lu[v] * dsu[v]) / su[v] : 0.0;
-                    if (av) {
-                        amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
-                                               fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                        for (int i = 0; i < NX; ++i) L.G[(size_t)lane * NX * GS + i * GS + NB] = -rp[i];
                     }
-                }
-                const double a_aff = wave_min(amax);
-                double mua_l = 0.0;
+                    WSYNC();
+                    TPHASE(4);
+                    if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
+                    TPHASE(6);
+                    riccati_forward(L, H, lane);
+                    TPHASE(3);
+                    double dd[NB], dp[NX];
+                    recover_step(L, H, lane, dd, dp);
+                    double amax = 1.0, mua_l = 0.0;
 #pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    if (av)
-                        mua_l += (ll[v] + a_aff * dll[v]) * (sl[v] + a_aff * dsl[v]) +
-                                 (lu[v] + a_aff * dlu[v]) * (su[v] + a_aff * dsu[v]);
-                }
-                const double mu_aff = wave_sum(mua_l) / nc;
-                const double sr = mu_aff / mu;
-                const double sigma = sr * sr * sr;
-                // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu
-                double rml[NB], rmu[NB];
-#pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    rml[v] = av ? ll[v] * sl[v] + dll[v] * dsl[v] - sigma * mu : 0.0;
-                    rmu[v] = av ? lu[v] * su[v] + dlu[v] * dsu[v] - sigma * mu : 0.0;
-                    if (on) L.gq[k * NB + v] = av ? rd[v] + (rml[v] + ll[v] * rl[v]) / sl[v] - (rmu[v] + lu[v] * ru[v]) / su[v] : 0.0;
-                }
-                WSYNC();
-                riccati_vector(L, H, lane);
-                riccati_forward(L, H, lane);
-                recover_step(L, H, lane, dd, dp);
-                amax = 1.0;
-#pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    dsl[v] = av ? dd[v] + rl[v] : 0.0;
-                    dsu[v] = av ? -dd[v] + ru[v] : 0.0;
-                    dll[v] = av ? (-rml[v] - ll[v] * dsl[v]) / sl[v] : 0.0;
-                    dlu[v] = av ? (-rmu[v] - lu[v] * dsu[v]) / su[v] : 0.0;
-                    if (av) {
-                        amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
-                                               fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                    for (int v = 0; v < NB; ++v) {
+                        const bool av = v < NX ? act_x : act_u;
+                        if (av) {
+                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
+                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
+                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
+                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
+                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
+                            amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl), max_step(su[v], dsu)),
+                                                   fmin(max_step(ll[v], dll), max_step(lu[v], dlu))));
+                        }
                     }
-                }
-                const double alpha = fmin(1.0, 0.995 * wave_min(amax));
+                    const double a_aff = wave_min(amax);
 #pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    const bool av = v < NX ? act_x : act_u;
-                    if (av) {
-                        d[v] = fma(alpha, dd[v], d[v]);
-                        sl[v] = fma(alpha, dsl[v], sl[v]);
-                        su[v] = fma(alpha, dsu[v], su[v]);
-                        ll[v] = fma(alpha, dll[v], ll[v]);
-                        lu[v] = fma(alpha, dlu[v], lu[v]);
+                    for (int v = 0; v < NB; ++v) {
+                        const bool av = v < NX ? act_x : act_u;
+                        if (av) {
+                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
+                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
+                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
+                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
+                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
+                            mua_l += (ll[v] + a_aff * dll) * (sl[v] + a_aff * dsl) + (lu[v] + a_aff * dlu) * (su[v] + a_aff * dsu);
+                        }
                     }
-                }
-                if (act_u) {
+                    const double mu_aff = wave_sum(mua_l) / nc;
+                    const double sr = mu_aff / mu;
+                    const double smu = sr * sr * sr * mu;
+                    // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu  ->  gq += (dll dsl - smu)/sl - (dlu dsu - smu)/su
+                    double dda[NB];
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
+                    for (int v = 0; v < NB; ++v) {
+                        dda[v] = dd[v];
+                        const bool av = v < NX ? act_x : act_u;
+                        if (on && av) {
+                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
+                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
+                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
+                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
+                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
+                            L.gq[k * NB + v] += (dll * dsl - smu) / sl[v] - (dlu * dsu - smu) / su[v];
+                        }
+                    }
+                    WSYNC();
+                    TPHASE(5);
+                    riccati_vector(L, H, lane);
+                    TPHASE(6);
+                    riccati_forward(L, H, lane);
+                    TPHASE(3);
+                    recover_step(L, H, lane, dd, dp);
+                    amax = 1.0;
+                    double dsl[NB], dsu[NB], dll[NB], dlu[NB];
+#pragma unroll
+                    for (int v = 0; v < NB; ++v) {
+                        const bool av = v < NX ? act_x : act_u;
+                        dsl[v] = dsu[v] = dll[v] = dlu[v] = 0.0;
+                        if (av) {
+                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
+                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
+                            const double dsla = dda[v] + rl, dsua = -dda[v] + ru;
+                            const double dlla = -ll[v] - ll[v] * dsla / sl[v];
+                            const double dlua = -lu[v] - lu[v] * dsua / su[v];
+                            const double rml = ll[v] * sl[v] + dlla * dsla - smu;
+                            const double rmu = lu[v] * su[v] + dlua * dsua - smu;
+                            dsl[v] = dd[v] + rl;
+                            dsu[v] = -dd[v] + ru;
+                            dll[v] = (-rml - ll[v] * dsl[v]) / sl[v];
+                            dlu[v] = (-rmu - lu[v] * dsu[v]) / su[v];
+                            amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
+                                                   fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                        }
+                    }
+                    const double alpha = fmin(1.0, 0.995 * wave_min(amax));
+#pragma unroll
+                    for (int v = 0; v < NB; ++v) {
+                        const bool av = v < NX ? act_x : act_u;
+                        if (av) {
+                            d[v] = fma(alpha, dd[v], d[v]);
+                            sl[v] = fma(alpha, dsl[v], sl[v]);
+                            su[v] = fma(alpha, dsu[v], su[v]);
+                            ll[v] = fma(alpha, dll[v], ll[v]);
+                            lu[v] = fma(alpha, dlu[v], lu[v]);
+                        }
+                    }
+                    if (act_u) {
+#pragma unroll
+                        for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
+                    }
                 }
             }
             qp_total += qit;
+            TPHASE(2);
             if (!qp_ok) { status = kQPFailure; break; }
             // full SQP step: w += d, multipliers <- QP multipliers
             bool fin = true;
@@ -860,7 +973,11 @@ struct SqpKernel {
             }
             if (wave_min(fin ? 1.0 : 0.0) < 0.5) { status = kNaN; break; }
         }
-
+        TPHASE(7);
+#ifdef GPMPC_TIMING
+        if (lane == 0 && io.timing != nullptr)
+            for (int q = 0; q < 8; ++q) io.timing[(size_t)b * 8 + q] = tacc[q];
+#endif
         // ---------------- write back (acados memory + x_prev/u_prev, gpmpc.py:366-368)
         double* xo = S.x + (size_t)b * (H + 1) * NX;
         double* uo = S.u + (size_t)b * H * NU;

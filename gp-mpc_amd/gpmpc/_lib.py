@@ -40,6 +40,9 @@ SIGNATURES = {
     "gpmpc_gp_predict": (_I, [_P, _I, _P, _I, _P, _P, _I, _P]),
     "gpmpc_gp_posterior": (_I, [_I, _I, _I, _P, _P, _D, _D, _D, _P, _I, _P, _P, _I, _P]),
     "gpmpc_plant_step": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
+    "gpmpc_set_profiling": (_I, [_P, _I]),
+    "gpmpc_kernel_times": (_I, [_P, POINTER(_D), POINTER(_I), POINTER(_D), POINTER(_I)]),
+    "gpmpc_set_timing_buffer": (_I, [_P, _P]),
     "gpmpc_lds_bytes": (c_int64, [_I, _I]),
 }
 

@@ -142,6 +142,17 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_tightening(self._h, 1, inverse_cdf(prob, self.nx), Ad.ctypes.data,
                                                  Bd.ctypes.data, K.ctypes.data))
 
+    def set_profiling(self, enabled: bool):
+        _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))
+
+    def kernel_times(self) -> dict:
+        """Summed HIP-event milliseconds of the variance / SQP kernels since the last call."""
+        vm, sm = ctypes.c_double(), ctypes.c_double()
+        vn, sn = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.gpmpc_kernel_times(self._h, ctypes.byref(vm), ctypes.byref(vn), ctypes.byref(sm),
+                                               ctypes.byref(sn)))
+        return {"var_ms": vm.value, "var_launches": vn.value, "sqp_ms": sm.value, "sqp_launches": sn.value}
+
     # ------------------------------------------------------------------ stepping
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream

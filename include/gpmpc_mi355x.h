@@ -136,6 +136,16 @@ gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double
 gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* params, const double* x,
                               const double* u, double* x_next, int32_t* tstep, void* stream);
 
+/* Kernel timing with HIP events recorded on the solve stream around the variance kernel
+ * and the SQP kernel of every gpmpc_solve while enabled.  gpmpc_kernel_times synchronises
+ * on the recorded events, returns the summed milliseconds and launch counts, and clears them. */
+gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled);
+gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp);
+
+/* Diagnostic builds (-DGPMPC_TIMING) only: device buffer [max_batch][8] (uint64) receiving
+ * per-phase shader-clock cycles of each instance's last solve; NULL disables. */
+gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
+
 /* LDS bytes one instance's workgroup needs (capacity planning / tests). */
 int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon);
 

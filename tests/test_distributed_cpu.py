@@ -1,0 +1,68 @@
+"""world_size-2 gloo test of the sharding / replication / reduction logic used by bench.py."""
+
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch.multiprocessing as mp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    sys.path[:0] = [str(ROOT / "gp-mpc_amd"), str(ROOT)]
+    import torch
+    import torch.distributed as dist
+
+    from gpmpc import distributed as D
+    from gpmpc.models import get_spec
+    from gpmpc.synthetic import initial_states, make_training_data
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    spec = get_spec("quad2d")
+    # rank 1 starts from a different seed: replication must overwrite it with rank 0's data
+    data = make_training_data(spec, 16, seed=1 if rank == 0 else 99)
+    rep = D.replicate_training_data(data)
+    ids = list(D.shard_range(8, rank))
+    x0, ph = initial_states(spec, spec.reference_trajectory(), 8 * world)
+    mine = torch.tensor(ph[ids[0]:ids[-1] + 1], dtype=torch.int64)
+    gathered = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(gathered, mine)
+    t = D.max_over_ranks([float(rank + 1), 1.0])
+    s = D.sum_over_ranks(torch.ones(3, dtype=torch.float64))
+    out.put((rank, [x.tolist() for x, _ in rep], [y.tolist() for _, y in rep], torch.cat(gathered).tolist(), t,
+             s.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_and_replication():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, x0, y0, g0, t0, s0), (_, x1, y1, g1, t1, s1) = res
+    assert x0 == x1 and y0 == y1                       # GP replicas identical after the broadcast
+    assert g0 == g1 == list(range(16))                 # 2 x 8 instances, contiguous, no overlap
+    assert t0 == t1 == [2.0, 1.0]                      # max over ranks
+    assert s0 == s1 == [2.0, 2.0, 2.0]
+    from gpmpc.models import get_spec
+    from gpmpc.synthetic import make_training_data
+
+    ref = make_training_data(get_spec("quad2d"), 16, seed=1)
+    np.testing.assert_array_equal(np.array(x0[0]), ref[0][0])

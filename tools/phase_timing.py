@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the SQP kernel with the diagnostic build (in-kernel s_memtime stamps).
+
+    make -C gp-mpc_amd/csrc timing && python tools/phase_timing.py [--model quad2d --batch 1024]
+
+Prints the mean shader-clock cycles per instance spent in each phase of one closed-loop
+step (after warm-up), and the share of the step.  Diagnostic only: the stamps themselves
+perturb the kernel; read the shares, not the absolute time.
+"""
+
+import argparse
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+os.environ.setdefault("GPMPC_LIB", str(ROOT / "gp-mpc_amd" / "gpmpc" / "lib" / "libgpmpc_mi355x_timing.so"))
+sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PHASES = ["tighten", "linearize", "resid/setup", "ipm-vector", "ric-factor", "ric-vector", "forward", "other"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="quad2d")
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--n-train", type=int, default=200)
+    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=5)
+    args = ap.parse_args()
+    from gpmpc import _lib
+    from gpmpc.gp import GaussianProcess
+    from gpmpc.models import get_spec
+    from gpmpc.solver import BatchSolver, setup_prior_dynamics
+    from gpmpc.synthetic import DEFAULT_HYPERS, initial_states, make_training_data
+
+    spec = get_spec(args.model)
+    H, B, N = args.horizon, args.batch, args.n_train
+    data = make_training_data(spec, N, seed=1)
+    gps = []
+    for i, (X, y) in enumerate(data):
+        gp = GaussianProcess(torch.tensor(X), torch.tensor(y))
+        gp.set_hyperparameters(*DEFAULT_HYPERS[spec.name][i])
+        gps.append(gp)
+    dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
+    mats = setup_prior_dynamics(dfdx, dfdu, np.diag(spec.q_diag), np.diag(spec.r_diag), spec.dt)
+    s = BatchSolver(spec, H, B)
+    s.set_gps(gps)
+    s.set_tightening(True, 0.95, *mats)
+    s.reset(True)
+    tbuf = torch.zeros(B, 8, dtype=torch.int64, device="cuda")
+    _lib.check(s.lib.gpmpc_set_timing_buffer(s._h, tbuf.data_ptr()))
+    traj = spec.reference_trajectory()
+    x0, ph = initial_states(spec, traj, B)
+    obs = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    for _ in range(args.warmup):
+        u0 = s.solve(obs, ts)
+        s.plant_step(obs, u0, ts, out=obs)
+    tot = np.zeros(8)
+    s.set_profiling(True)
+    s.kernel_times()
+    for _ in range(args.steps):
+        u0 = s.solve(obs, ts)
+        torch.cuda.synchronize()
+        tot += tbuf.cpu().numpy().mean(0)
+        s.plant_step(obs, u0, ts, out=obs)
+    kt = s.kernel_times()
+    cyc = tot / args.steps
+    ms = kt["sqp_ms"] / max(kt["sqp_launches"], 1)
+    print(f"{spec.name} B={B} H={H} N={N}: sqp kernel {ms:.3f} ms/launch, sqp_iter {s.sqp_iter.float().mean():.2f}, "
+          f"qp_iter {s.qp_iter.float().mean():.2f}")
+    print(f"cycles per instance (mean) {cyc.sum():.0f} -> {cyc.sum() / (ms * 1e-3) / 1e9:.2f} G cycles/s effective")
+    for name, c in zip(PHASES, cyc):
+        print(f"  {name:12s} {c:12.0f} cycles  {100 * c / cyc.sum():5.1f} %")
+
+
+if __name__ == "__main__":
+    main()
