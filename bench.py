@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--qp-tol", type=float, default=1e-10, help="IPM tolerance of the QP sub-problems")
+    ap.add_argument("--qp-mu0", type=float, default=1.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,7 +138,7 @@ def main():
     dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
     lqr_mats = setup_prior_dynamics(dfdx, dfdu, Q, R, spec.dt)
 
-    solver = BatchSolver(spec, H, B, device=dev)
+    solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
     solver.set_gps(gps)
     solver.set_tightening(True, 0.95, *lqr_mats)
     solver.reset(reset_iterate=True)

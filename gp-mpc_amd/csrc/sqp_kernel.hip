@@ -53,6 +53,28 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)bits, l);
+    const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// 1/x to full double precision: v_rcp_f64 estimate + two Newton steps (no IEEE div sequence)
+__device__ __forceinline__ double fast_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
 // In-register inverse of a small SPD matrix (Gauss-Jordan, no pivoting needed for SPD).
 template <int N>
 __device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][N]) {
@@ -65,7 +87,7 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][
     for (int c = 0; c < N; ++c) {
         const double piv = a[c][c];
         ok = ok && (piv > 0.0);
-        const double r = 1.0 / piv;
+        const double r = fast_rcp(piv);
 #pragma unroll
         for (int j = 0; j < N; ++j) { a[c][j] *= r; inv[c][j] *= r; }
 #pragma unroll
@@ -136,35 +158,53 @@ struct SqpKernel {
     static constexpr int N3 = N3P + NU * PS;                 // + K'_k
     static constexpr int R1 = (N1 + 63) / 64, R2 = (N2 + 63) / 64, R3 = (N3 + 63) / 64;
 
+    // Riccati on v_mfma_f64_16x16x4 when every stage product fits one 16x16 tile
+    // (G' has NB+1 <= 16 columns, the forward state [dx; 1] has NX+1 <= 8 rows).
+    static constexpr bool kMfma = (NB + 1 <= 16) && (NX + 1 <= 8);
+    static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
+
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy;
     };
+    __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
     __host__ __device__ static size_t lds_doubles(int H) {
-        return (size_t)H * NX * GS           // G'_k
-               + (size_t)(H + 1) * NX * PS   // P'_k
-               + (size_t)H * NU * PS         // K'_k
-               + (size_t)H * NU * NU         // Ru_k^-1
-               + (size_t)(H + 1) * NB * 2    // hq, gq
-               + (size_t)(H + 1) * NX        // dx (forward sweep)
-               + (size_t)NX * GS + GS * GS + 2 * NB + NX  // W', M', vectors
-               + (size_t)H * NUNC            // cov_d diag per stage
-               + (size_t)2 * NX * NX + NU * NX;  // Sigma, T scratch
+        const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
+                              + (size_t)H * NX * GS            // G'_k
+                              + (size_t)H * NU * PS          // K'_k
+                              + (size_t)H * NU * NU          // Ru_k^-1
+                              + (size_t)(H + 1) * NB * 2     // hq, gq
+                              + (size_t)(H + 1) * NX;        // dx (forward sweep)
+        if (kMfma) {
+            const size_t acl = (size_t)H * NX * PS;            // closed-loop A'_k (tightening scratch aliases it)
+            return common + (size_t)(H + 1) * PP + (acl > tight_scratch(H) ? acl : tight_scratch(H));
+        }
+        return common + (size_t)(H + 1) * NX * PS              // P'_k
+               + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
+               + tight_scratch(H);
     }
     __device__ static Lds carve(double* s, int H) {
-        Lds L;
+        Lds L{};
+        L.dummy = s; s += 64;
         L.G = s;   s += (size_t)H * NX * GS;
-        L.P = s;   s += (size_t)(H + 1) * NX * PS;
         L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
         L.hq = s;  s += (size_t)(H + 1) * NB;
         L.gq = s;  s += (size_t)(H + 1) * NB;
         L.dxv = s; s += (size_t)(H + 1) * NX;
-        L.W = s;   s += (size_t)NX * GS;
-        L.Ms = s;  s += (size_t)GS * GS;
-        L.vs = s;  s += (size_t)2 * NB + NX;
-        L.cd = s;  s += (size_t)H * NUNC;
-        L.Sig = s;
+        if (kMfma) {
+            L.P = s;   s += (size_t)(H + 1) * PP;
+            L.Acl = s;
+            L.cd = s;
+            L.Sig = s + (size_t)H * NUNC;
+        } else {
+            L.P = s;   s += (size_t)(H + 1) * NX * PS;
+            L.W = s;   s += (size_t)NX * GS;
+            L.Ms = s;  s += (size_t)GS * GS;
+            L.vs = s;  s += (size_t)2 * NB + NX;
+            L.cd = s;  s += (size_t)H * NUNC;
+            L.Sig = s;
+        }
         return L;
     }
 
@@ -589,6 +629,235 @@ struct SqpKernel {
         }
     }
 
+    // ------------------------------------------------------------------ Riccati on MFMA (NB+1 <= 16)
+    // Tile conventions of v_mfma_f64_16x16x4_f64 (lane l, lr = l>>4, lc = l&15):
+    //   A operand of K-step s: A[lc][4s+lr];  B operand: B[4s+lr][lc];  C/D register r: D[lr+4r][lc].
+    // A matrix held in C layout is therefore directly the B operand of the next product, and
+    // a SYMMETRIC matrix in C layout is also its own A operand.  P (symmetric) stays in
+    // registers from stage to stage; per stage:
+    //   W = P G' (+ p on column NB)      2 MFMAs, B = G' rows (LDS)
+    //   M = G'^T W + [diag(hq) | gq]     2 MFMAs, A = the same G' registers, B = W registers
+    //   Schur onto the state block       Ru by readlane, row/column slices by lane shuffles
+    __device__ static int pidx(int i, int j) { return i * NX - (i * (i - 1)) / 2 + (j - i); }  // i <= j < NX
+
+    __device__ static bool mfma_backward(const Lds& L, int H, int lane, bool vector_only) {
+        const int lr = lane >> 4, lc = lane & 15;
+        const bool colok = (lc < NX) || (lc == NB);
+        const int jj = (lc == NB) ? NX : lc;
+        double pn[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int row = lr + 4 * r;
+            double v = 0.0;
+            if (row < NX) {
+                if (lc < NX) v = (row == lc) ? L.hq[H * NB + row] : 0.0;
+                else if (lc == NB) v = L.gq[H * NB + row];
+            }
+            pn[r] = v;
+        }
+        {   // P'_H (packed) for the multiplier recovery of stage H-1
+            double* PH = L.P + (size_t)H * PP;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int row = lr + 4 * r;
+                if (row < NX) {
+                    if (lc == NB) PH[NX * (NX + 1) / 2 + row] = pn[r];
+                    else if (!vector_only && lc < NX && row <= lc) PH[pidx(row, lc)] = pn[r];
+                }
+            }
+        }
+        bool ok = true;
+        // stage data of stage k (loaded one stage ahead so the LDS latency hides under the MFMAs)
+        auto load_stage = [&](int k, double (&gc)[2], f64x4& dinit) {
+            const double* G = L.G + (size_t)k * NX * GS;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int row = lr + 4 * s2;
+                gc[s2] = (row < NX && lc < GS) ? G[row * GS + lc] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = lr + 4 * r;
+                const bool dg = row < NB && row == lc, gcol = row < NB && lc == NB;
+                const double v = (dg ? L.hq : L.gq)[(dg || gcol) ? k * NB + row : 0];
+                dinit[r] = (dg || gcol) ? v : 0.0;
+            }
+        };
+        double gcn[2];
+        f64x4 dinitn;
+        load_stage(H - 1, gcn, dinitn);
+        for (int k = H - 1; k >= 0; --k) {
+            double gc[2] = {gcn[0], gcn[1]};
+            const f64x4 dinit = dinitn;
+            if (k > 0) load_stage(k - 1, gcn, dinitn);
+            const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, 0.0, 0.0};
+            f64x4 w = mfma64(lc < NX ? pn[0] : 0.0, gc[0], cw);
+            w = mfma64(lc < NX ? pn[1] : 0.0, gc[1], w);
+            f64x4 m = mfma64(gc[0], w[0], dinit);
+            m = mfma64(gc[1], w[1], m);
+            double Ri[NU][NU];
+            if (!vector_only) {
+                double Ru[NU][NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int b2 = a; b2 < NU; ++b2) {
+                        const int ra = NX + a, cb = NX + b2;
+                        Ru[a][b2] = readlane_d(m[ra >> 2], ((ra & 3) << 4) | cb);
+                        Ru[b2][a] = Ru[a][b2];
+                    }
+                if constexpr (NU == 1) {
+                    ok = ok && (Ru[0][0] > 0.0);
+                    Ri[0][0] = fast_rcp(Ru[0][0]);
+                } else if constexpr (NU == 2) {
+                    const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
+                    ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
+                    const double id = fast_rcp(det);
+                    Ri[0][0] = Ru[1][1] * id;
+                    Ri[1][1] = Ru[0][0] * id;
+                    Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
+                } else {
+                    ok = spd_inverse<NU>(Ru, Ri) && ok;
+                }
+                if (lane < NU * NU) {
+                    double rv = 0.0;
+#pragma unroll
+                    for (int a = 0; a < NU; ++a)
+#pragma unroll
+                        for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
+                    L.Rui[(size_t)k * NU * NU + lane] = rv;
+                }
+            } else {
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int b2 = 0; b2 < NU; ++b2) Ri[a][b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
+            }
+            double mcol[NU], tr[NU];
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                const int rr = NX + b2;
+                mcol[b2] = __shfl(m[rr >> 2], ((rr & 3) << 4) | lc);
+            }
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                double t = 0.0;
+#pragma unroll
+                for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], mcol[b2], t);
+                tr[a] = t;
+            }
+            double* Pk = L.P + (size_t)k * PP;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                double acc = m[r];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) acc = fma(-__shfl(m[r], (lane & 48) | (NX + a)), tr[a], acc);
+                const int row = lr + 4 * r;
+                const bool valid = (row < NX) && colok;
+                // branch-free store: entries that are not stored go to a dummy slot
+                const bool st = valid && ((lc == NB) || (!vector_only && row <= lc));
+                const int idx = (lc == NB) ? NX * (NX + 1) / 2 + row : pidx(row < lc ? row : lc, row < lc ? lc : row);
+                (st ? Pk : L.dummy)[st ? idx : lane] = acc;
+                pn[r] = valid ? acc : 0.0;
+            }
+            {
+                const bool st = lr == 0 && colok && (!vector_only || lc == NB);
+                double* Kk = st ? L.K + (size_t)k * NU * PS + jj : L.dummy + lane;
+#pragma unroll
+                for (int a = 0; a < NU; ++a) Kk[st ? a * PS : 0] = -tr[a];
+            }
+        }
+        return ok;
+    }
+
+    // Closed-loop stage maps A'_k = [A + B K | B kff + c] (all stages in parallel); only the
+    // affine column when the factorisation is unchanged (corrector).
+    __device__ static void acl_phase(const Lds& L, int H, int lane, bool full) {
+        const int cols = full ? PS : 1;
+        const int n = H * NX * cols;
+        for (int e = lane; e < n; e += 64) {
+            const int k = e / (NX * cols);
+            const int rem = e - k * NX * cols;
+            const int i = rem / cols;
+            const int j = full ? rem - i * cols : NX;
+            const double* G = L.G + (size_t)k * NX * GS + i * GS;
+            const double* Kk = L.K + (size_t)k * NU * PS;
+            double acc = (j < NX) ? G[j] : G[NB];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc = fma(G[NX + a], Kk[a * PS + j], acc);
+            L.Acl[(size_t)k * NX * PS + i * PS + j] = acc;
+        }
+    }
+
+    // Forward sweep on MFMA: X_{k+1} = A'_k [dx_k; 1] with X held in column 0 of a C tile,
+    // which is also the B operand of the next stage's product.
+    __device__ static void mfma_forward(const Lds& L, int H, int lane) {
+        const int lr = lane >> 4, lc = lane & 15;
+        double xb[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) xb[s2] = (lc == 0 && lr + 4 * s2 == NX) ? 1.0 : 0.0;
+        if (lane < NX) L.dxv[lane] = 0.0;
+        auto load_stage = [&](int k, double (&a)[2]) {
+            const double* A = L.Acl + (size_t)k * NX * PS;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int col = lr + 4 * s2;
+                const bool ok = lc < NX && col < PS;
+                const double v = A[ok ? lc * PS + col : 0];
+                a[s2] = ok ? v : 0.0;
+            }
+        };
+        double an[2];
+        load_stage(0, an);
+        for (int k = 0; k < H; ++k) {
+            double a[2] = {an[0], an[1]};
+            if (k + 1 < H) load_stage(k + 1, an);
+            f64x4 acc = mfma64(a[0], xb[0], f64x4{0.0, 0.0, 0.0, 0.0});
+            acc = mfma64(a[1], xb[1], acc);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int row = lr + 4 * s2;
+                xb[s2] = (lc == 0) ? (row < NX ? acc[s2] : (row == NX ? 1.0 : 0.0)) : 0.0;
+                if (lc == 0 && row < NX) L.dxv[(size_t)(k + 1) * NX + row] = acc[s2];
+            }
+        }
+    }
+
+    // Per-lane step from the MFMA Riccati solution (packed P').
+    __device__ static void recover_step_mfma(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        const bool on = lane <= H;
+        const int kk = min(lane, H - 1);
+        double dx[NX], dxn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            dx[i] = (on && lane >= 1) ? L.dxv[(size_t)lane * NX + i] : 0.0;
+            dxn[i] = L.dxv[(size_t)(kk + 1) * NX + i];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dd[i] = dx[i];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double kr[PS];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) kr[j] = L.K[(size_t)kk * NU * PS + a * PS + j];
+            double du = kr[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) du = fma(kr[j], dx[j], du);
+            dd[NX + a] = (lane < H) ? du : 0.0;
+        }
+        const double* Pn = L.P + (size_t)(kk + 1) * PP;
+        double pp[PP];
+#pragma unroll
+        for (int q = 0; q < PP; ++q) pp[q] = Pn[q];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = pp[NX * (NX + 1) / 2 + i];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(pp[i <= j ? pidx(i, j) : pidx(j, i)], dxn[j], acc);
+            dpi[i] = (lane < H) ? -acc : 0.0;
+        }
+    }
+
     // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
     __device__ static void ctpi(const Lds& L, int H, int lane, const double (&pi)[NX], double (&out)[NB]) {
         double pim1[NX];
@@ -744,7 +1013,7 @@ struct SqpKernel {
         auto lbv = [&](int v) { return (v < NX ? P.x_lo[v] : P.u_lo[v - NX]) + tsd[v] - P.uh; };
         auto ubv = [&](int v) { return (v < NX ? P.x_hi[v] : P.u_hi[v - NX]) - tsd[v] + P.uh; };
 
-        const Entries E = decode(lane);
+        [[maybe_unused]] const Entries E = decode(lane);
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
         const double nc = 2.0 * (double)H * (double)NB;
         int status = kMaxIter, it = 0, qp_total = 0;
@@ -853,12 +1122,24 @@ struct SqpKernel {
                     }
                     WSYNC();
                     TPHASE(4);
-                    if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
-                    TPHASE(6);
-                    riccati_forward(L, H, lane);
-                    TPHASE(3);
                     double dd[NB], dp[NX];
-                    recover_step(L, H, lane, dd, dp);
+                    if constexpr (kMfma) {
+                        if (!mfma_backward(L, H, lane, false)) { qp_ok = false; break; }
+                        WSYNC();
+                        acl_phase(L, H, lane, true);
+                        WSYNC();
+                        TPHASE(6);
+                        mfma_forward(L, H, lane);
+                        WSYNC();
+                        TPHASE(3);
+                        recover_step_mfma(L, H, lane, dd, dp);
+                    } else {
+                        if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
+                        TPHASE(6);
+                        riccati_forward(L, H, lane);
+                        TPHASE(3);
+                        recover_step(L, H, lane, dd, dp);
+                    }
                     double amax = 1.0, mua_l = 0.0;
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
@@ -906,11 +1187,23 @@ struct SqpKernel {
                     }
                     WSYNC();
                     TPHASE(5);
-                    riccati_vector(L, H, lane);
-                    TPHASE(6);
-                    riccati_forward(L, H, lane);
-                    TPHASE(3);
-                    recover_step(L, H, lane, dd, dp);
+                    if constexpr (kMfma) {
+                        mfma_backward(L, H, lane, true);
+                        WSYNC();
+                        acl_phase(L, H, lane, false);
+                        WSYNC();
+                        TPHASE(6);
+                        mfma_forward(L, H, lane);
+                        WSYNC();
+                        TPHASE(3);
+                        recover_step_mfma(L, H, lane, dd, dp);
+                    } else {
+                        riccati_vector(L, H, lane);
+                        TPHASE(6);
+                        riccati_forward(L, H, lane);
+                        TPHASE(3);
+                        recover_step(L, H, lane, dd, dp);
+                    }
                     amax = 1.0;
                     double dsl[NB], dsu[NB], dll[NB], dlu[NB];
 #pragma unroll
