@@ -102,7 +102,7 @@ def main():
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--qp-tol", type=float, default=1e-10, help="IPM tolerance of the QP sub-problems")
+    ap.add_argument("--qp-tol", type=float, default=1e-8, help="IPM tolerance of the QP sub-problems")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
     args = ap.parse_args()
 

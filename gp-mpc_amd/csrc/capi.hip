@@ -169,8 +169,8 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.tighten = 0;
     P.max_iter = 25;          // gpmpc.py:262
     P.tol_stat = P.tol_eq = P.tol_ineq = P.tol_comp = 1e-6;  // acados defaults
-    P.qp_max_iter = 100;
-    P.qp_tol = 1e-10;
+    P.qp_max_iter = 50;   // acados qp_solver_iter_max default
+    P.qp_tol = 1e-8;     // HPIPM default residual tolerances (acados leaves qp_tol unset, gpmpc.py:257-263)
     P.qp_mu0 = 1.0;
     const size_t lds = sqp_lds_bytes(model_id, horizon);
     if (lds > 160 * 1024) {

@@ -4,13 +4,16 @@
 //                   var(z) = sf2 - || L^-1 k(z, X) ||^2 (+ sn2)        (gpmpc/gpmpc.py:441-445)
 //   The variance is the dense contraction of the path: V = K_ZX (P x N) * L^-T (N x N,
 //   upper triangular) on v_mfma_f64_16x16x4_f64, A-operand tiles generated on the fly
-//   (one exp per lane per K-step), triangular K-steps skipped, and the squared row norms
-//   reduced in registers.  One wavefront = 16 points; 4 wavefronts per workgroup.
+//   (one exp per lane per K-step), B panels staged in LDS and shared by the workgroup,
+//   the zero triangle skipped, squared row norms reduced in registers.  One wavefront =
+//   16 points; 8 wavefronts per workgroup.
 //
 //   plant_step_kernel: one RK4 step of the prior-only dynamics with the "true" parameters --
 //   the synthetic closed-loop plant that replaces crazyflow's env.step (scripts/run_gp_mpc.py:59).
 #include "gpmpc_common.h"
 #include "models.h"
+
+#include <type_traits>
 
 namespace gpmpc {
 
@@ -34,82 +37,137 @@ __device__ __forceinline__ void load_point(const PostArgs& a, int p, double (&z)
     }
 }
 
-constexpr int kColTiles = 8;  // 128 output columns per pass over K
+// ---------------------------------------------------------------------------- posterior
+// Workgroup = 8 wavefronts = 128 points.  (L^-1)^T streams through LDS in 16-row panels
+// (double-buffered, register-staged global loads), shared by the 8 waves: each panel row
+// feeds 8 x 16 points.  Column tiles of one pass stay in accumulators (<= kMaxCT tiles =
+// 256 columns; larger N loops over column groups and regenerates the kernel values).
+// Only the upper triangle is loaded and multiplied.  The LDS row stride is an odd number of
+// 16-column tiles so the four k-rows of a B fragment hit disjoint bank halves.
+constexpr int kPostWaves = 8;
+constexpr int kMaxCT = 16;
+
+__device__ __forceinline__ double dpp_row_sum(double v) {
+    auto mv = [](double x, auto ctrl) {
+        const long long b = __double_as_longlong(x);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)b, decltype(ctrl)::value, 0xf, 0xf, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), decltype(ctrl)::value, 0xf, 0xf, false);
+        return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    };
+    v += mv(v, std::integral_constant<int, 0x128>{});   // row_ror:8
+    v += mv(v, std::integral_constant<int, 0x124>{});   // row_ror:4
+    v += mv(v, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
+    v += mv(v, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+    return v;
+}
+
+__host__ __device__ inline int post_ct(int npad) { return npad / 16 < kMaxCT ? npad / 16 : kMaxCT; }
+__host__ __device__ inline int post_stride(int ct) { return 16 * (ct | 1); }
 
 template <bool FROM_STATE>
-__global__ __launch_bounds__(256) void gp_post_kernel(GPDev g, int npad, PostArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int p0 = (blockIdx.x * 4 + wave) * 16;
-    if (p0 >= a.P) return;
-    const int prow = lane & 15;   // A-operand row (point) of this lane
-    const int kq = lane >> 4;     // A-operand k / B-operand k of this lane
-    const int p = p0 + prow;
+__global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(GPDev g, int npad, PostArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double panel[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lc = lane & 15;   // A-operand row (point) / B-operand column of this lane
+    const int kq = lane >> 4;   // k index within a K-step
+    const int p0 = (blockIdx.x * kPostWaves + wave) * 16;
+    const int p = p0 + lc;
     const bool pvalid = p < a.P;
     double z[3];
-    load_point<FROM_STATE>(a, pvalid ? p : p0, z);
+    load_point<FROM_STATE>(a, pvalid ? p : a.P - 1, z);
     const double c = -0.5 * g.inv_ell2;
     const double4* rows = reinterpret_cast<const double4*>(g.vrows);
-    const int nsteps = npad / 4;
     double msum = 0.0;
-    double sq[4] = {0.0, 0.0, 0.0, 0.0};
-    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr);
-    const int ngroups = want_var ? (npad + 16 * kColTiles - 1) / (16 * kColTiles) : 1;
-    for (int grp = 0; grp < ngroups; ++grp) {
-        const int c0 = grp * 16 * kColTiles;
-        f64x4 acc[kColTiles];
+    auto kval = [&](int i, bool acc_mean) {
+        double kv = 0.0;
+        if (i < g.nv) {
+            const double4 r = rows[i];
+            const double xr[3] = {r.x, r.y, r.z};
+            double q = 0.0;
 #pragma unroll
-        for (int t = 0; t < kColTiles; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-        // K-steps needed by this column group: i <= last column (L^-T upper triangular)
-        const int last_col = min(npad, c0 + 16 * kColTiles) - 1;
-        const int s_end = want_var ? min(nsteps, last_col / 4 + 1) : nsteps;
-        for (int s = 0; s < s_end; ++s) {
-            const int i = 4 * s + kq;
-            double kv = 0.0;
-            if (i < g.nv && pvalid) {
-                const double4 r = rows[i];
-                const double xr[3] = {r.x, r.y, r.z};
-                double q = 0.0;
-#pragma unroll
-                for (int dd = 0; dd < 3; ++dd) {
-                    const double df = (dd < g.d) ? xr[dd] - z[dd] : 0.0;
-                    q = fma(df, df, q);
-                }
-                kv = g.sf2 * exp(c * q);
-                if (grp == ngroups - 1) msum = fma(kv, r.w, msum);  // the last group spans every K-step
+            for (int dd = 0; dd < 3; ++dd) {
+                const double df = (dd < g.d) ? xr[dd] - z[dd] : 0.0;
+                q = fma(df, df, q);
             }
-            if (want_var) {
-                const double* brow = g.linvT + (size_t)i * npad + c0 + (lane & 15);
-#pragma unroll
-                for (int t = 0; t < kColTiles; ++t) {
-                    const int col0 = c0 + 16 * t;
-                    if (col0 < npad && 4 * s <= col0 + 15) {   // wave-uniform: skip zero triangle
-                        const double bv = brow[16 * t];
-                        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv, bv, acc[t], 0, 0, 0);
-                    }
-                }
-            }
+            kv = g.sf2 * exp(c * q);
+            if (acc_mean) msum = fma(kv, r.w, msum);
         }
-        if (want_var) {
-            // acc[t][r] = V[row = kq + 4r][col = c0 + 16t + (lane&15)]
+        return kv;
+    };
+    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr);
+    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+    if (!want_var) {
+        for (int s = 0; s < npad / 4; ++s) (void)kval(4 * s + kq, true);
+    } else {
+        const int ntile = npad / 16;
+        const int ct = post_ct(npad);
+        const int Wp = post_stride(ct);
+        const int ngroups = (ntile + ct - 1) / ct;
+        for (int grp = 0; grp < ngroups; ++grp) {
+            const int t0 = grp * ct;
+            const int tn = min(ct, ntile - t0);
+            const int npan = t0 + tn;                       // K rows < 16 (t0 + tn): upper triangle
+            const bool last = grp == ngroups - 1;           // the last group visits every K row
+            // staged copy of panel `pan` (columns of tiles >= max(pan, t0) of this group)
+            double2 stage[4];
+            auto fetch = [&](int pan) {
+                const int lt0 = max(pan - t0, 0), w = 16 * (tn - lt0);
 #pragma unroll
-            for (int t = 0; t < kColTiles; ++t)
+                for (int j = 0; j < 4; ++j) {
+                    const int e = 2 * (tid + j * 64 * kPostWaves);
+                    const int row = e / w, col = e - row * w;
+                    stage[j] = (row < 16)
+                                   ? *reinterpret_cast<const double2*>(g.linvT + (size_t)(16 * pan + row) * npad +
+                                                                       16 * (t0 + lt0) + col)
+                                   : double2{0.0, 0.0};
+                }
+            };
+            auto deposit = [&](int pan, double* buf) {
+                const int lt0 = max(pan - t0, 0), w = 16 * (tn - lt0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) sq[r] = fma(acc[t][r], acc[t][r], sq[r]);
+                for (int j = 0; j < 4; ++j) {
+                    const int e = 2 * (tid + j * 64 * kPostWaves);
+                    const int row = e / w, col = e - row * w;
+                    if (row < 16) *reinterpret_cast<double2*>(buf + row * Wp + 16 * lt0 + col) = stage[j];
+                }
+            };
+            f64x4 acc[kMaxCT];
+#pragma unroll
+            for (int t = 0; t < kMaxCT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+            fetch(0);
+            deposit(0, panel);
+            __syncthreads();
+            for (int pan = 0; pan < npan; ++pan) {
+                const double* buf = panel + (pan & 1) * 16 * Wp;
+                if (pan + 1 < npan) fetch(pan + 1);
+                const int lt0 = max(pan - t0, 0);
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const double kv = kval(16 * pan + 4 * ks + kq, last);
+                    const double* brow = buf + (4 * ks + kq) * Wp + lc;
+#pragma unroll
+                    for (int t = 0; t < kMaxCT; ++t)
+                        if (t >= lt0 && t < tn) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv, brow[16 * t], acc[t], 0, 0, 0);
+                }
+                if (pan + 1 < npan) deposit(pan + 1, panel + ((pan + 1) & 1) * 16 * Wp);
+                __syncthreads();
+            }
+            // acc[t][r] = V[point kq + 4r][column 16 (t0 + t) + lc]
+#pragma unroll
+            for (int t = 0; t < kMaxCT; ++t)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sq[r] = (t < tn) ? fma(acc[t][r], acc[t][r], sq[r]) : sq[r];
         }
     }
-    // mean: reduce the 4 k-lanes of each point (lanes prow, prow+16, prow+32, prow+48)
+    // mean: reduce the 4 k-lanes of each point (lanes lc, lc+16, lc+32, lc+48)
     msum += __shfl_xor(msum, 16);
     msum += __shfl_xor(msum, 32);
     if (a.mean != nullptr && kq == 0 && pvalid) a.mean[p] = msum;
     if (want_var) {
-        // reduce squared norms over the 16 column lanes sharing kq
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) sq[r] += __shfl_xor(sq[r], o);
-        }
-        if ((lane & 15) == 0) {
+        for (int r = 0; r < 4; ++r) sq[r] = dpp_row_sum(sq[r]);   // over the 16 column lanes
+        if (lc == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int pr = p0 + kq + 4 * r;
@@ -123,13 +181,23 @@ __global__ __launch_bounds__(256) void gp_post_kernel(GPDev g, int npad, PostArg
 }
 
 hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream) {
-    const int waves = (a.P + 15) / 16;
-    const int blocks = (waves + 3) / 4;
+    const int blocks = (a.P + 16 * kPostWaves - 1) / (16 * kPostWaves);
     if (blocks == 0) return hipSuccess;
+    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr);
+    const size_t lds = want_var ? (size_t)2 * 16 * post_stride(post_ct(npad)) * sizeof(double) : 0;
+    static bool attr = false;
+    if (!attr) {
+        const int mx = 2 * 16 * post_stride(kMaxCT) * (int)sizeof(double);
+        hipError_t e = hipFuncSetAttribute((const void*)gp_post_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)gp_post_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
     if (from_state)
-        hipLaunchKernelGGL(gp_post_kernel<true>, dim3(blocks), dim3(256), 0, stream, g, npad, a);
+        hipLaunchKernelGGL(gp_post_kernel<true>, dim3(blocks), dim3(64 * kPostWaves), lds, stream, g, npad, a);
     else
-        hipLaunchKernelGGL(gp_post_kernel<false>, dim3(blocks), dim3(256), 0, stream, g, npad, a);
+        hipLaunchKernelGGL(gp_post_kernel<false>, dim3(blocks), dim3(64 * kPostWaves), lds, stream, g, npad, a);
     return hipGetLastError();
 }
 

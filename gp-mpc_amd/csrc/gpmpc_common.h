@@ -10,6 +10,7 @@ constexpr int kMaxGPDim = 3;    // inputs per GP (packed rows are 4 doubles: x0,
 constexpr int kMaxNX = 12;
 constexpr int kMaxNU = 4;
 constexpr int kMaxH = 63;       // one lane per stage 0..H (64-lane wavefront)
+constexpr int kPhases = 12;  // diagnostic phase slots (GPMPC_TIMING builds)
 constexpr int kMaxParams = 16;
 
 enum ModelId : int32_t { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };

@@ -23,8 +23,9 @@ namespace gpmpc {
 #define WSYNC() __syncthreads()  // block == one wavefront: orders LDS traffic of the wave
 
 // Diagnostic phase timing (build with -DGPMPC_TIMING): shader-clock cycles per phase,
-// accumulated by the wave and stored per instance.  Phases: 0 tightening, 1 linearise,
-// 2 residuals/QP setup, 3 IPM vector work, 4 Riccati factor, 5 Riccati vector, 6 forward sweeps.
+// accumulated by the wave and stored per instance.  Phases (kPhases): 0 tightening, 1 linearise,
+// 2 residuals/QP setup, 3 IPM vector work, 4 Riccati factor, 5 Riccati vector, 6 forward sweeps,
+// 7 other, 8 closed-loop maps, 9 step recovery, 10 IPM residuals/Newton data.
 #ifdef GPMPC_TIMING
 #define TPHASE(id)                                                   \
     do {                                                             \
@@ -37,20 +38,52 @@ namespace gpmpc {
 #define TPHASE(id) do { } while (0)
 #endif
 
+// ------------------------------------------------------------------ cross-lane moves (gfx950)
+// Butterfly partners without the LDS crossbar: DPP row rotations / quad permutes inside a
+// 16-lane row, v_permlane16_swap / v_permlane32_swap across rows.  With vdst == src0 the swap
+// instructions return the partner lane l^16 (l^32) in one of their two results.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double xor16_d(double v) {   // value of lane l ^ 16
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const bool odd = threadIdx.x & 16;
+    const unsigned int rl = odd ? lo[0] : lo[1], rh = odd ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)rh << 32) | rl);
+}
+__device__ __forceinline__ double xor32_d(double v) {   // value of lane l ^ 32
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    const bool up = threadIdx.x & 32;
+    const unsigned int rl = up ? lo[0] : lo[1], rh = up ? hi[0] : hi[1];
+    return __longlong_as_double(((long long)rh << 32) | rl);
+}
+// Whole-wave reductions (all 64 lanes active).  Every lane ends with the bitwise-same value:
+// each step combines a lane with a partner holding the mirrored partial (commutative ops).
+template <class Op>
+__device__ __forceinline__ double wave_reduce(double v, Op op) {
+    v = op(v, dpp_d<0x128>(v));   // row_ror:8
+    v = op(v, dpp_d<0x124>(v));   // row_ror:4
+    v = op(v, dpp_d<0x4E>(v));    // quad_perm [2,3,0,1]
+    v = op(v, dpp_d<0xB1>(v));    // quad_perm [1,0,3,2]
+    v = op(v, xor16_d(v));
+    return op(v, xor32_d(v));
+}
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
+    return wave_reduce(v, [](double a, double b) { return fmax(a, b); });
 }
 __device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
+    return wave_reduce(v, [](double a, double b) { return fmin(a, b); });
 }
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    return wave_reduce(v, [](double a, double b) { return a + b; });
 }
 
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -640,10 +673,15 @@ struct SqpKernel {
     //   Schur onto the state block       Ru by readlane, row/column slices by lane shuffles
     __device__ static int pidx(int i, int j) { return i * NX - (i * (i - 1)) / 2 + (j - i); }  // i <= j < NX
 
-    __device__ static bool mfma_backward(const Lds& L, int H, int lane, bool vector_only) {
+    __device__ static bool mfma_backward(const Lds& L, int H, int lane) {
         const int lr = lane >> 4, lc = lane & 15;
         const bool colok = (lc < NX) || (lc == NB);
         const int jj = (lc == NB) ? NX : lc;
+        // rows NX..NX+NU-1 of the C tile (the u rows of M') sit in element SE of lane groups
+        // SG..SG+NU-1; the Schur operands need them in lane groups 0..NU-1.
+        constexpr int SE = NX >> 2, SG = NX & 3;
+        static_assert(((NX + NU - 1) >> 2) == SE && SG + NU <= 4, "u rows of M' must share one C element");
+        static_assert(NU <= 2, "MFMA Schur path handles NU <= 2");
         double pn[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -662,7 +700,7 @@ struct SqpKernel {
                 const int row = lr + 4 * r;
                 if (row < NX) {
                     if (lc == NB) PH[NX * (NX + 1) / 2 + row] = pn[r];
-                    else if (!vector_only && lc < NX && row <= lc) PH[pidx(row, lc)] = pn[r];
+                    else if (lc < NX && row <= lc) PH[pidx(row, lc)] = pn[r];
                 }
             }
         }
@@ -690,81 +728,75 @@ struct SqpKernel {
             double gc[2] = {gcn[0], gcn[1]};
             const f64x4 dinit = dinitn;
             if (k > 0) load_stage(k - 1, gcn, dinitn);
+            // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
             const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, 0.0, 0.0};
             f64x4 w = mfma64(lc < NX ? pn[0] : 0.0, gc[0], cw);
             w = mfma64(lc < NX ? pn[1] : 0.0, gc[1], w);
             f64x4 m = mfma64(gc[0], w[0], dinit);
             m = mfma64(gc[1], w[1], m);
+            // Ru = M'_uu by readlane, closed-form inverse
             double Ri[NU][NU];
-            if (!vector_only) {
+            {
                 double Ru[NU][NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a)
 #pragma unroll
                     for (int b2 = a; b2 < NU; ++b2) {
-                        const int ra = NX + a, cb = NX + b2;
-                        Ru[a][b2] = readlane_d(m[ra >> 2], ((ra & 3) << 4) | cb);
+                        Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
                         Ru[b2][a] = Ru[a][b2];
                     }
                 if constexpr (NU == 1) {
                     ok = ok && (Ru[0][0] > 0.0);
                     Ri[0][0] = fast_rcp(Ru[0][0]);
-                } else if constexpr (NU == 2) {
+                } else {
                     const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
                     ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
                     const double id = fast_rcp(det);
                     Ri[0][0] = Ru[1][1] * id;
                     Ri[1][1] = Ru[0][0] * id;
                     Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
-                } else {
-                    ok = spd_inverse<NU>(Ru, Ri) && ok;
                 }
-                if (lane < NU * NU) {
-                    double rv = 0.0;
-#pragma unroll
-                    for (int a = 0; a < NU; ++a)
-#pragma unroll
-                        for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
-                    L.Rui[(size_t)k * NU * NU + lane] = rv;
-                }
-            } else {
+            }
+            if (lane < NU * NU) {
+                double rv = 0.0;
 #pragma unroll
                 for (int a = 0; a < NU; ++a)
 #pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) Ri[a][b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
+                    for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
+                L.Rui[(size_t)k * NU * NU + lane] = rv;
             }
-            double mcol[NU], tr[NU];
-#pragma unroll
-            for (int b2 = 0; b2 < NU; ++b2) {
-                const int rr = NX + b2;
-                mcol[b2] = __shfl(m[rr >> 2], ((rr & 3) << 4) | lc);
+            // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry)
+            double mu;
+            if constexpr (SG == 0) mu = m[SE];
+            else if constexpr (SG == 2) mu = xor32_d(m[SE]);
+            else mu = __shfl(m[SE], (((lr + SG) & 3) << 4) | lc);
+            // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff)
+            double kb;
+            if constexpr (NU == 1) {
+                kb = -Ri[0][0] * mu;
+            } else {
+                const double mo = xor16_d(mu);
+                const bool odd = lr & 1;
+                const double m0 = odd ? mo : mu, m1 = odd ? mu : mo;
+                kb = -fma(odd ? Ri[1][0] : Ri[0][0], m0, (odd ? Ri[1][1] : Ri[0][1]) * m1);
             }
-#pragma unroll
-            for (int a = 0; a < NU; ++a) {
-                double t = 0.0;
-#pragma unroll
-                for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], mcol[b2], t);
-                tr[a] = t;
-            }
+            kb = (lr < NU) ? kb : 0.0;
+            // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M')
+            const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);
             double* Pk = L.P + (size_t)k * PP;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                double acc = m[r];
-#pragma unroll
-                for (int a = 0; a < NU; ++a) acc = fma(-__shfl(m[r], (lane & 48) | (NX + a)), tr[a], acc);
                 const int row = lr + 4 * r;
                 const bool valid = (row < NX) && colok;
                 // branch-free store: entries that are not stored go to a dummy slot
-                const bool st = valid && ((lc == NB) || (!vector_only && row <= lc));
+                const bool st = valid && ((lc == NB) || row <= lc);
                 const int idx = (lc == NB) ? NX * (NX + 1) / 2 + row : pidx(row < lc ? row : lc, row < lc ? lc : row);
-                (st ? Pk : L.dummy)[st ? idx : lane] = acc;
-                pn[r] = valid ? acc : 0.0;
+                (st ? Pk : L.dummy)[st ? idx : lane] = pk[r];
+                pn[r] = valid ? pk[r] : 0.0;
             }
             {
-                const bool st = lr == 0 && colok && (!vector_only || lc == NB);
-                double* Kk = st ? L.K + (size_t)k * NU * PS + jj : L.dummy + lane;
-#pragma unroll
-                for (int a = 0; a < NU; ++a) Kk[st ? a * PS : 0] = -tr[a];
+                const bool st = lr < NU && colok;
+                (st ? L.K : L.dummy)[st ? (size_t)k * NU * PS + lr * PS + jj : lane] = kb;
             }
         }
         return ok;
@@ -821,6 +853,112 @@ struct SqpKernel {
                 if (lc == 0 && row < NX) L.dxv[(size_t)(k + 1) * NX + row] = acc[s2];
             }
         }
+    }
+
+    // Forward sweep on the VALU: dx_{k+1} = A'_k [dx_k; 1], lane i < NX owns dx[i] and the state
+    // is broadcast with v_readlane (scalar operands), so the chain has no MFMA output->operand
+    // latency and no LDS round trip; the rows of A'_{k+1} are fetched one stage ahead.
+    __device__ static void valu_forward(const Lds& L, int H, int lane) {
+        const int row = lane < NX ? lane : 0;
+        double x = 0.0;
+        if (lane < NX) L.dxv[lane] = 0.0;
+        auto load = [&](int k, double (&a)[PS]) {
+            const double* A = L.Acl + (size_t)k * NX * PS + row * PS;
+#pragma unroll
+            for (int j = 0; j < PS; ++j) a[j] = A[j];
+        };
+        double an[PS];
+        load(0, an);
+        for (int k = 0; k < H; ++k) {
+            double a[PS];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) a[j] = an[j];
+            if (k + 1 < H) load(k + 1, an);
+            double acc0 = a[NX], acc1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                if (j & 1) acc1 = fma(a[j], readlane_d(x, j), acc1);
+                else acc0 = fma(a[j], readlane_d(x, j), acc0);
+            }
+            x = acc0 + acc1;
+            if (lane < NX) L.dxv[(size_t)(k + 1) * NX + lane] = x;
+        }
+    }
+
+    // Corrector right-hand side with the factorisation unchanged (the Riccati "solve" of HPIPM):
+    //   p_k = vt_k + A_cl,k^T p_{k+1},  vt_k = q_k + K_k^T r_k + A_cl,k^T P_{k+1} c_k,  p_H = q_H,
+    //   kff_k = -Ru_k^-1 (r_k + B_k^T (P_{k+1} c_k + p_{k+1})),
+    // with [q; r] = gq.  Only the p recurrence is sequential (6-term VALU dot products with
+    // readlane broadcast); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
+    // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
+    __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
+        constexpr int PO = NX * (NX + 1) / 2;
+        double* T = L.hq;
+        double* VT = L.dxv;
+        for (int e = lane; e < H * NX; e += 64) {
+            const int k = e / NX, i = e - k * NX;
+            const double* Pn = L.P + (size_t)(k + 1) * PP;
+            const double* G = L.G + (size_t)k * NX * GS;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
+            T[e] = acc;
+        }
+        WSYNC();
+        for (int e = lane; e < H * NX; e += 64) {
+            const int k = e / NX, i = e - k * NX;
+            const double* A = L.Acl + (size_t)k * NX * PS;
+            const double* Kk = L.K + (size_t)k * NU * PS;
+            double acc = L.gq[k * NB + i];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * PS + i], L.gq[k * NB + NX + a], acc);
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
+            VT[e] = acc;
+        }
+        WSYNC();
+        const int col = lane < NX ? lane : 0;
+        double p = L.gq[H * NB + col];
+        if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
+        auto load = [&](int k, double (&ac)[NX], double& vt) {
+            const double* A = L.Acl + (size_t)k * NX * PS + col;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) ac[l] = A[l * PS];
+            vt = VT[k * NX + col];
+        };
+        double acn[NX], vtn;
+        load(H - 1, acn, vtn);
+        for (int k = H - 1; k >= 0; --k) {
+            double ac[NX];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) ac[l] = acn[l];
+            const double vt = vtn;
+            if (k > 0) load(k - 1, acn, vtn);
+            double acc0 = vt, acc1 = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                if (l & 1) acc1 = fma(ac[l], readlane_d(p, l), acc1);
+                else acc0 = fma(ac[l], readlane_d(p, l), acc0);
+            }
+            p = acc0 + acc1;
+            if (lane < NX) L.P[(size_t)k * PP + PO + lane] = p;
+        }
+        WSYNC();
+        for (int e = lane; e < H * NU; e += 64) {
+            const int k = e / NU, a = e - k * NU;
+            const double* G = L.G + (size_t)k * NX * GS;
+            const double* pn = L.P + (size_t)(k + 1) * PP + PO;
+            double kf = 0.0;
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                double acc = L.gq[k * NB + NX + b2];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + NX + b2], T[k * NX + l] + pn[l], acc);
+                kf = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], acc, kf);
+            }
+            L.K[(size_t)k * NU * PS + a * PS + NX] = -kf;
+        }
+        WSYNC();
     }
 
     // Per-lane step from the MFMA Riccati solution (packed P').
@@ -917,7 +1055,7 @@ struct SqpKernel {
         const bool act_u = lane < H;
         const int k = min(lane, H);
 #ifdef GPMPC_TIMING
-        unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long tacc[kPhases] = {};
         unsigned long long tlast = __builtin_amdgcn_s_memtime();
         int tcur = 7;
 #endif
@@ -1088,6 +1226,7 @@ struct SqpKernel {
             TPHASE(3);
             for (qit = 0; qit < P.qp_max_iter; ++qit) {
                 double rp[NX];
+                TPHASE(10);
                 {
                     double ctq[NB];
                     ctpi(L, H, lane, piq, ctq);
@@ -1124,15 +1263,17 @@ struct SqpKernel {
                     TPHASE(4);
                     double dd[NB], dp[NX];
                     if constexpr (kMfma) {
-                        if (!mfma_backward(L, H, lane, false)) { qp_ok = false; break; }
+                        if (!mfma_backward(L, H, lane)) { qp_ok = false; break; }
                         WSYNC();
+                        TPHASE(8);
                         acl_phase(L, H, lane, true);
                         WSYNC();
                         TPHASE(6);
-                        mfma_forward(L, H, lane);
+                        valu_forward(L, H, lane);
                         WSYNC();
-                        TPHASE(3);
+                        TPHASE(9);
                         recover_step_mfma(L, H, lane, dd, dp);
+                        TPHASE(3);
                     } else {
                         if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
                         TPHASE(6);
@@ -1188,15 +1329,16 @@ struct SqpKernel {
                     WSYNC();
                     TPHASE(5);
                     if constexpr (kMfma) {
-                        mfma_backward(L, H, lane, true);
-                        WSYNC();
+                        valu_vector_backward(L, H, lane);
+                        TPHASE(8);
                         acl_phase(L, H, lane, false);
                         WSYNC();
                         TPHASE(6);
-                        mfma_forward(L, H, lane);
+                        valu_forward(L, H, lane);
                         WSYNC();
-                        TPHASE(3);
+                        TPHASE(9);
                         recover_step_mfma(L, H, lane, dd, dp);
+                        TPHASE(3);
                     } else {
                         riccati_vector(L, H, lane);
                         TPHASE(6);
@@ -1269,7 +1411,7 @@ struct SqpKernel {
         TPHASE(7);
 #ifdef GPMPC_TIMING
         if (lane == 0 && io.timing != nullptr)
-            for (int q = 0; q < 8; ++q) io.timing[(size_t)b * 8 + q] = tacc[q];
+            for (int q = 0; q < kPhases; ++q) io.timing[(size_t)b * kPhases + q] = tacc[q];
 #endif
         // ---------------- write back (acados memory + x_prev/u_prev, gpmpc.py:366-368)
         double* xo = S.x + (size_t)b * (H + 1) * NX;

@@ -57,7 +57,7 @@ class BatchSolver:
 
     def __init__(self, spec: ModelSpec, horizon: int, batch: int, device="cuda", prior_params: dict | None = None,
                  traj: np.ndarray | None = None, uh: float = -1e-8, cost_scaling: bool = True, max_iter: int = 25,
-                 tol: float = 1e-6, qp_max_iter: int = 100, qp_tol: float = 1e-10, qp_mu0: float = 1.0):
+                 tol: float = 1e-6, qp_max_iter: int = 50, qp_tol: float = 1e-8, qp_mu0: float = 1.0):
         self.lib = _lib.load()
         self.spec = spec
         self.H = int(horizon)
@@ -97,7 +97,7 @@ class BatchSolver:
             self._h = None
 
     # ------------------------------------------------------------------ configuration
-    def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=100, qp_tol=1e-10, qp_mu0=1.0):
+    def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=50, qp_tol=1e-8, qp_mu0=1.0):
         _lib.check(self.lib.gpmpc_set_options(self._h, int(max_iter), tol, tol, tol, tol, int(qp_max_iter), qp_tol, qp_mu0))
 
     def set_reference(self, traj: np.ndarray):

@@ -142,7 +142,7 @@ gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* para
 gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled);
 gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp);
 
-/* Diagnostic builds (-DGPMPC_TIMING) only: device buffer [max_batch][8] (uint64) receiving
+/* Diagnostic builds (-DGPMPC_TIMING) only: device buffer [max_batch][12] (uint64) receiving
  * per-phase shader-clock cycles of each instance's last solve; NULL disables. */
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
 

@@ -71,7 +71,7 @@ def test_closed_loop_parity(name, N, H, B, steps):
     gpp = product_gps(data, hyp)
     mats = lqr(spec)
     tol = 1e-9
-    solver = BatchSolver(spec, H, B, tol=tol)
+    solver = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)  # tight KKT for parity
     solver.set_gps(gpp)
     solver.set_tightening(True, 0.95, *mats)
     solver.reset(reset_iterate=True)

@@ -20,7 +20,8 @@ sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-PHASES = ["tighten", "linearize", "resid/setup", "ipm-vector", "ric-factor", "ric-vector", "forward", "other"]
+PHASES = ["tighten", "linearize", "resid/setup", "ipm-vector", "ric-factor", "ric-vector", "forward", "other",
+          "acl-maps", "recover", "ipm-resid", "-"]
 
 
 def main():
@@ -52,7 +53,7 @@ def main():
     s.set_gps(gps)
     s.set_tightening(True, 0.95, *mats)
     s.reset(True)
-    tbuf = torch.zeros(B, 8, dtype=torch.int64, device="cuda")
+    tbuf = torch.zeros(B, len(PHASES), dtype=torch.int64, device="cuda")
     _lib.check(s.lib.gpmpc_set_timing_buffer(s._h, tbuf.data_ptr()))
     traj = spec.reference_trajectory()
     x0, ph = initial_states(spec, traj, B)
@@ -61,7 +62,7 @@ def main():
     for _ in range(args.warmup):
         u0 = s.solve(obs, ts)
         s.plant_step(obs, u0, ts, out=obs)
-    tot = np.zeros(8)
+    tot = np.zeros(len(PHASES))
     s.set_profiling(True)
     s.kernel_times()
     for _ in range(args.steps):
