@@ -386,8 +386,10 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             e1 = take_event(h);
             if (e0) HIPCHK(hipEventRecord(e0, s));
         }
+        PostBatch pb{};
+        pb.n = h->md.ngp;
         for (int g = 0; g < h->md.ngp; ++g) {
-            PostArgs a{};
+            PostArgs& a = pb.a[g];
             a.sx = h->x;
             a.su = h->u;
             a.H = h->H;
@@ -403,8 +405,10 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             a.var = h->var;
             a.var_stride = h->md.ngp;
             a.var_off = g;
-            HIPCHK(launch_gp_post(P.gp[g], h->gp_npad[g], a, true, s));
+            pb.g[g] = P.gp[g];
+            pb.npad[g] = h->gp_npad[g];
         }
+        HIPCHK(launch_gp_post_batch(pb, true, s));
         if (e0 && e1) {
             HIPCHK(hipEventRecord(e1, s));
             h->ev_var.push_back({e0, e1});

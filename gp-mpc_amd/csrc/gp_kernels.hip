@@ -6,13 +6,14 @@
 //   upper triangular) on v_mfma_f64_16x16x4_f64, A-operand tiles generated on the fly
 //   (one exp per lane per K-step), B panels staged in LDS and shared by the workgroup,
 //   the zero triangle skipped, squared row norms reduced in registers.  One wavefront =
-//   16 points; 8 wavefronts per workgroup.
+//   16 points; 8 wavefronts per workgroup; all GPs of a step in one launch (grid.y).
 //
 //   plant_step_kernel: one RK4 step of the prior-only dynamics with the "true" parameters --
 //   the synthetic closed-loop plant that replaces crazyflow's env.step (scripts/run_gp_mpc.py:59).
 #include "gpmpc_common.h"
 #include "models.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace gpmpc {
@@ -65,8 +66,12 @@ __host__ __device__ inline int post_ct(int npad) { return npad / 16 < kMaxCT ? n
 __host__ __device__ inline int post_stride(int ct) { return 16 * (ct | 1); }
 
 template <bool FROM_STATE>
-__global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(GPDev g, int npad, PostArgs a) {
+__global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) {
     extern __shared__ __attribute__((aligned(16))) double panel[];
+    const GPDev& g = pb.g[blockIdx.y];
+    const PostArgs& a = pb.a[blockIdx.y];
+    const int npad = pb.npad[blockIdx.y];
+    if ((int)blockIdx.x * kPostWaves * 16 >= a.P) return;   // whole workgroup past the end (uniform)
     const int tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int lc = lane & 15;   // A-operand row (point) / B-operand column of this lane
@@ -142,9 +147,12 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(GPDev g, int n
                 const double* buf = panel + (pan & 1) * 16 * Wp;
                 if (pan + 1 < npan) fetch(pan + 1);
                 const int lt0 = max(pan - t0, 0);
+                double kvs[4];   // the panel's four kernel values first: independent exps (ILP)
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) kvs[ks] = kval(16 * pan + 4 * ks + kq, last);
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
-                    const double kv = kval(16 * pan + 4 * ks + kq, last);
+                    const double kv = kvs[ks];
                     const double* brow = buf + (4 * ks + kq) * Wp + lc;
 #pragma unroll
                     for (int t = 0; t < kMaxCT; ++t)
@@ -180,11 +188,15 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(GPDev g, int n
     }
 }
 
-hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream) {
-    const int blocks = (a.P + 16 * kPostWaves - 1) / (16 * kPostWaves);
-    if (blocks == 0) return hipSuccess;
-    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr);
-    const size_t lds = want_var ? (size_t)2 * 16 * post_stride(post_ct(npad)) * sizeof(double) : 0;
+hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream) {
+    int blocks = 0;
+    size_t lds = 0;
+    for (int q = 0; q < pb.n; ++q) {
+        blocks = max(blocks, (pb.a[q].P + 16 * kPostWaves - 1) / (16 * kPostWaves));
+        if (pb.a[q].var != nullptr && pb.g[q].linvT != nullptr)
+            lds = std::max(lds, (size_t)2 * 16 * post_stride(post_ct(pb.npad[q])) * sizeof(double));
+    }
+    if (blocks == 0 || pb.n == 0) return hipSuccess;
     static bool attr = false;
     if (!attr) {
         const int mx = 2 * 16 * post_stride(kMaxCT) * (int)sizeof(double);
@@ -195,10 +207,19 @@ hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from
         attr = true;
     }
     if (from_state)
-        hipLaunchKernelGGL(gp_post_kernel<true>, dim3(blocks), dim3(64 * kPostWaves), lds, stream, g, npad, a);
+        hipLaunchKernelGGL(gp_post_kernel<true>, dim3(blocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
     else
-        hipLaunchKernelGGL(gp_post_kernel<false>, dim3(blocks), dim3(64 * kPostWaves), lds, stream, g, npad, a);
+        hipLaunchKernelGGL(gp_post_kernel<false>, dim3(blocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
     return hipGetLastError();
+}
+
+hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream) {
+    PostBatch pb{};
+    pb.g[0] = g;
+    pb.a[0] = a;
+    pb.npad[0] = npad;
+    pb.n = 1;
+    return launch_gp_post_batch(pb, from_state, stream);
 }
 
 // ---------------------------------------------------------------------------- plant

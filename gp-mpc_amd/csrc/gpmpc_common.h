@@ -97,10 +97,19 @@ struct PostArgs {
     int32_t var_stride, var_off;
 };
 
+// Up to kMaxGP posterior evaluations in one launch (grid.y = GP).
+struct PostBatch {
+    GPDev g[kMaxGP];
+    PostArgs a[kMaxGP];
+    int32_t npad[kMaxGP];
+    int32_t n;
+};
+
 // Launchers (sqp_kernel.hip, gp_kernels.hip).
 hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream);
 size_t sqp_lds_bytes(int model, int H);
 hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream);
+hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream);
 hipError_t launch_plant(int model, const double* params, double dt, const double* x, const double* u, double* xn,
                         int32_t* tstep, int B, hipStream_t stream);
 

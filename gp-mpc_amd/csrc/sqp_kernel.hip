@@ -198,11 +198,12 @@ struct SqpKernel {
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero;
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
     __host__ __device__ static size_t lds_doubles(int H) {
         const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
+                              + (size_t)8                    // zero slots (branch-free masked loads)
                               + (size_t)H * NX * GS            // G'_k
                               + (size_t)H * NU * PS          // K'_k
                               + (size_t)H * NU * NU          // Ru_k^-1
@@ -219,6 +220,7 @@ struct SqpKernel {
     __device__ static Lds carve(double* s, int H) {
         Lds L{};
         L.dummy = s; s += 64;
+        L.zero = s;  s += 8;
         L.G = s;   s += (size_t)H * NX * GS;
         L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
@@ -682,6 +684,7 @@ struct SqpKernel {
         constexpr int SE = NX >> 2, SG = NX & 3;
         static_assert(((NX + NU - 1) >> 2) == SE && SG + NU <= 4, "u rows of M' must share one C element");
         static_assert(NU <= 2, "MFMA Schur path handles NU <= 2");
+        static_assert(NB <= 8 && NX <= 8, "stage operands occupy C elements 0..1");
         double pn[2];
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
@@ -705,35 +708,44 @@ struct SqpKernel {
             }
         }
         bool ok = true;
-        // stage data of stage k (loaded one stage ahead so the LDS latency hides under the MFMAs)
-        auto load_stage = [&](int k, double (&gc)[2], f64x4& dinit) {
-            const double* G = L.G + (size_t)k * NX * GS;
+        // Stage operands as per-lane (base, stride) streams: lanes whose entry is structurally zero
+        // read the zero slot with stride 0, so a stage load is one address step and no select.
+        // G'_k row r (< NX), column lc (< GS) -> B operand of W' / A operand of M'.
+        const double* gb[2];
+        int gst[2];
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int row = lr + 4 * s2;
-                gc[s2] = (row < NX && lc < GS) ? G[row * GS + lc] : 0.0;
-            }
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int row = lr + 4 * s2;
+            const bool ok2 = row < NX && lc < GS;
+            gb[s2] = ok2 ? L.G + row * GS + lc : L.zero;
+            gst[s2] = ok2 ? NX * GS : 0;
+        }
+        // C-init of M': hq on the diagonal (rows < NB), gq in column NB
+        const double* db[2];
+        int dst[2];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = lr + 4 * r;
-                const bool dg = row < NB && row == lc, gcol = row < NB && lc == NB;
-                const double v = (dg ? L.hq : L.gq)[(dg || gcol) ? k * NB + row : 0];
-                dinit[r] = (dg || gcol) ? v : 0.0;
+        for (int r = 0; r < 2; ++r) {
+            const int row = lr + 4 * r;
+            const bool dg = row < NB && row == lc, gcol = row < NB && lc == NB;
+            db[r] = dg ? L.hq + row : (gcol ? L.gq + row : L.zero);
+            dst[r] = (dg || gcol) ? NB : 0;
+        }
+        struct Stage { double g[2], d[2]; };
+        auto load_stage = [&](int k, Stage& st) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                st.g[q] = gb[q][k * gst[q]];
+                st.d[q] = db[q][k * dst[q]];
             }
         };
-        double gcn[2];
-        f64x4 dinitn;
-        load_stage(H - 1, gcn, dinitn);
-        for (int k = H - 1; k >= 0; --k) {
-            double gc[2] = {gcn[0], gcn[1]};
-            const f64x4 dinit = dinitn;
-            if (k > 0) load_stage(k - 1, gcn, dinitn);
+        double* Pk = nullptr;
+        auto stage = [&](int k, const Stage& sd) {
             // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
             const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, 0.0, 0.0};
-            f64x4 w = mfma64(lc < NX ? pn[0] : 0.0, gc[0], cw);
-            w = mfma64(lc < NX ? pn[1] : 0.0, gc[1], w);
-            f64x4 m = mfma64(gc[0], w[0], dinit);
-            m = mfma64(gc[1], w[1], m);
+            f64x4 w = mfma64(lc < NX ? pn[0] : 0.0, sd.g[0], cw);
+            w = mfma64(lc < NX ? pn[1] : 0.0, sd.g[1], w);
+            f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], 0.0, 0.0});
+            m = mfma64(sd.g[1], w[1], m);
             // Ru = M'_uu by readlane, closed-form inverse
             double Ri[NU][NU];
             {
@@ -757,13 +769,14 @@ struct SqpKernel {
                     Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
                 }
             }
-            if (lane < NU * NU) {
+            {
                 double rv = 0.0;
 #pragma unroll
                 for (int a = 0; a < NU; ++a)
 #pragma unroll
                     for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
-                L.Rui[(size_t)k * NU * NU + lane] = rv;
+                const bool st = lane < NU * NU;
+                (st ? L.Rui : L.dummy)[st ? (size_t)k * NU * NU + lane : lane] = rv;
             }
             // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry)
             double mu;
@@ -783,7 +796,7 @@ struct SqpKernel {
             kb = (lr < NU) ? kb : 0.0;
             // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M')
             const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);
-            double* Pk = L.P + (size_t)k * PP;
+            Pk = L.P + (size_t)k * PP;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int row = lr + 4 * r;
@@ -798,7 +811,19 @@ struct SqpKernel {
                 const bool st = lr < NU && colok;
                 (st ? L.K : L.dummy)[st ? (size_t)k * NU * PS + lr * PS + jj : lane] = kb;
             }
+        };
+        // stage k's operands are loaded one stage ahead (explicit double buffer: no register
+        // copies that would force the wait right after the load)
+        Stage s0, s1;
+        load_stage(H - 1, s0);
+        int k = H - 1;
+        for (; k >= 1; k -= 2) {
+            load_stage(k - 1, s1);
+            stage(k, s0);
+            if (k >= 2) load_stage(k - 2, s0);
+            stage(k - 1, s1);
         }
+        if (k == 0) stage(0, s0);
         return ok;
     }
 
@@ -862,18 +887,14 @@ struct SqpKernel {
         const int row = lane < NX ? lane : 0;
         double x = 0.0;
         if (lane < NX) L.dxv[lane] = 0.0;
+        double* out = (lane < NX) ? L.dxv + NX + lane : L.dummy + lane;
+        const int ost = (lane < NX) ? NX : 0;
+        const double* arow = L.Acl + row * PS;
         auto load = [&](int k, double (&a)[PS]) {
-            const double* A = L.Acl + (size_t)k * NX * PS + row * PS;
 #pragma unroll
-            for (int j = 0; j < PS; ++j) a[j] = A[j];
+            for (int j = 0; j < PS; ++j) a[j] = arow[(size_t)k * NX * PS + j];
         };
-        double an[PS];
-        load(0, an);
-        for (int k = 0; k < H; ++k) {
-            double a[PS];
-#pragma unroll
-            for (int j = 0; j < PS; ++j) a[j] = an[j];
-            if (k + 1 < H) load(k + 1, an);
+        auto step = [&](int k, const double (&a)[PS]) {
             double acc0 = a[NX], acc1 = 0.0;
 #pragma unroll
             for (int j = 0; j < NX; ++j) {
@@ -881,8 +902,18 @@ struct SqpKernel {
                 else acc0 = fma(a[j], readlane_d(x, j), acc0);
             }
             x = acc0 + acc1;
-            if (lane < NX) L.dxv[(size_t)(k + 1) * NX + lane] = x;
+            out[k * ost] = x;
+        };
+        double a0[PS], a1[PS];
+        load(0, a0);
+        int k = 0;
+        for (; k + 1 < H; k += 2) {
+            load(k + 1, a1);
+            step(k, a0);
+            if (k + 2 < H) load(k + 2, a0);
+            step(k + 1, a1);
         }
+        if (k < H) step(k, a0);
     }
 
     // Corrector right-hand side with the factorisation unchanged (the Riccati "solve" of HPIPM):
@@ -920,29 +951,35 @@ struct SqpKernel {
         const int col = lane < NX ? lane : 0;
         double p = L.gq[H * NB + col];
         if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
-        auto load = [&](int k, double (&ac)[NX], double& vt) {
-            const double* A = L.Acl + (size_t)k * NX * PS + col;
+        double* out = (lane < NX) ? L.P + PO + lane : L.dummy + lane;
+        const int ost = (lane < NX) ? PP : 0;
+        const double* acol = L.Acl + col;
+        struct Col { double a[NX]; double vt; };
+        auto load = [&](int k, Col& c) {
 #pragma unroll
-            for (int l = 0; l < NX; ++l) ac[l] = A[l * PS];
-            vt = VT[k * NX + col];
+            for (int l = 0; l < NX; ++l) c.a[l] = acol[(size_t)k * NX * PS + l * PS];
+            c.vt = VT[k * NX + col];
         };
-        double acn[NX], vtn;
-        load(H - 1, acn, vtn);
-        for (int k = H - 1; k >= 0; --k) {
-            double ac[NX];
-#pragma unroll
-            for (int l = 0; l < NX; ++l) ac[l] = acn[l];
-            const double vt = vtn;
-            if (k > 0) load(k - 1, acn, vtn);
-            double acc0 = vt, acc1 = 0.0;
+        auto step = [&](int k, const Col& c) {
+            double acc0 = c.vt, acc1 = 0.0;
 #pragma unroll
             for (int l = 0; l < NX; ++l) {
-                if (l & 1) acc1 = fma(ac[l], readlane_d(p, l), acc1);
-                else acc0 = fma(ac[l], readlane_d(p, l), acc0);
+                if (l & 1) acc1 = fma(c.a[l], readlane_d(p, l), acc1);
+                else acc0 = fma(c.a[l], readlane_d(p, l), acc0);
             }
             p = acc0 + acc1;
-            if (lane < NX) L.P[(size_t)k * PP + PO + lane] = p;
+            out[k * ost] = p;
+        };
+        Col c0, c1;
+        load(H - 1, c0);
+        int k = H - 1;
+        for (; k >= 1; k -= 2) {
+            load(k - 1, c1);
+            step(k, c0);
+            if (k >= 2) load(k - 2, c0);
+            step(k - 1, c1);
         }
+        if (k == 0) step(0, c0);
         WSYNC();
         for (int e = lane; e < H * NU; e += 64) {
             const int k = e / NU, a = e - k * NU;
@@ -1050,6 +1087,7 @@ struct SqpKernel {
         const int b = blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve(smem, H);
+        if (lane < 8) L.zero[lane] = 0.0;   // read by the masked stage-operand streams
         const bool on = lane <= H;
         const bool act_x = on && lane >= 1;
         const bool act_u = lane < H;

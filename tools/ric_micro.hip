@@ -18,6 +18,7 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     const auto L = KQ::carve(smem, H);
     const int lane = threadIdx.x;
     constexpr int NX = KQ::NX, NB = KQ::NB, GS = KQ::GS, PS = KQ::PS;
+    if (lane < 8) L.zero[lane] = 0.0;
     // synthetic, well-conditioned stage data: G' = [I + 0.01 R | 0.1 R | 0.01], hq >= 1
     for (int e = lane; e < H * NX * GS; e += 64) {
         const int j = e % GS, i = (e / GS) % NX;
