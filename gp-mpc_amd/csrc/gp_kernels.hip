@@ -95,7 +95,7 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
                 const double df = (dd < g.d) ? xr[dd] - z[dd] : 0.0;
                 q = fma(df, df, q);
             }
-            kv = g.sf2 * exp(c * q);
+            kv = g.sf2 * exp_rbf(c * q);
             if (acc_mean) msum = fma(kv, r.w, msum);
         }
         return kv;

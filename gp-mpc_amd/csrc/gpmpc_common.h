@@ -97,6 +97,30 @@ struct PostArgs {
     int32_t var_stride, var_off;
 };
 
+// exp(x) for the RBF kernel, x <= 0 and finite: Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2,
+// degree-13 Taylor polynomial (truncation < 2e-17 relative), scale by 2^n with v_ldexp (which
+// flushes to 0 below the denormal range).  No overflow/NaN guards: the argument is -0.5 q/ell^2.
+__device__ __forceinline__ double exp_rbf(double x) {
+    const double n = __builtin_rint(x * 1.4426950408889634);
+    double r = fma(n, -6.93147180369123816490e-01, x);
+    r = fma(n, -1.90821492927058770002e-10, r);
+    double p = 1.6059043836821614599e-10;   // 1/13!
+    p = fma(p, r, 2.0876756987868098979e-09);
+    p = fma(p, r, 2.5052108385441718775e-08);
+    p = fma(p, r, 2.7557319223985890653e-07);
+    p = fma(p, r, 2.7557319223985890653e-06);
+    p = fma(p, r, 2.4801587301587301587e-05);
+    p = fma(p, r, 1.9841269841269841270e-04);
+    p = fma(p, r, 1.3888888888888888889e-03);
+    p = fma(p, r, 8.3333333333333333333e-03);
+    p = fma(p, r, 4.1666666666666666667e-02);
+    p = fma(p, r, 1.6666666666666666667e-01);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return __builtin_amdgcn_ldexp(p, (int)n);
+}
+
 // Up to kMaxGP posterior evaluations in one launch (grid.y = GP).
 struct PostBatch {
     GPDev g[kMaxGP];

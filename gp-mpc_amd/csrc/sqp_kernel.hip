@@ -136,41 +136,37 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][
 
 // Partial GP sums over training rows [i0, i1): m = sum alpha_i e_i, g_d = sum alpha_i e_i (x_id - z_d),
 // e_i = exp(-0.5 |z - x_i|^2 / ell^2)  (gpmpc/gp.py:12-14, 84-85; alpha = K^-1 y).
+// Rows are fetched one pair ahead so the L1/L2 latency hides under the previous pair's math.
 template <int D>
 __device__ __forceinline__ void gp_partial(const GPDev& g, const double* z, int i0, int i1, double& m, double (&gacc)[3]) {
     const double c = -0.5 * g.inv_ell2;
     double m0 = 0.0, m1 = 0.0;
     double a0[3] = {0, 0, 0}, a1[3] = {0, 0, 0};
     const double4* rows = reinterpret_cast<const double4*>(g.rows);
-    int i = i0;
-    for (; i + 1 < i1; i += 2) {
-        const double4 ra = rows[i], rb = rows[i + 1];
-        const double xa[3] = {ra.x, ra.y, ra.z}, xb[3] = {rb.x, rb.y, rb.z};
-        double qa = 0.0, qb = 0.0, da[3], db[3];
+    auto point = [&](const double4& r, double& msum, double (&acc)[3]) {
+        const double xr[3] = {r.x, r.y, r.z};
+        double q = 0.0, dv[3];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            da[d] = xa[d] - z[d];
-            db[d] = xb[d] - z[d];
-            qa = fma(da[d], da[d], qa);
-            qb = fma(db[d], db[d], qb);
+            dv[d] = xr[d] - z[d];
+            q = fma(dv[d], dv[d], q);
         }
-        const double wa = ra.w * exp(c * qa), wb = rb.w * exp(c * qb);
-        m0 += wa;
-        m1 += wb;
+        const double w = r.w * exp_rbf(c * q);
+        msum += w;
 #pragma unroll
-        for (int d = 0; d < D; ++d) { a0[d] = fma(wa, da[d], a0[d]); a1[d] = fma(wb, db[d], a1[d]); }
+        for (int d = 0; d < D; ++d) acc[d] = fma(w, dv[d], acc[d]);
+    };
+    const int last = max(i1 - 1, i0);
+    double4 ra = rows[min(i0, last)], rb = rows[min(i0 + 1, last)];
+    int i = i0;
+    for (; i + 1 < i1; i += 2) {
+        const double4 ca = ra, cb = rb;
+        ra = rows[min(i + 2, last)];
+        rb = rows[min(i + 3, last)];
+        point(ca, m0, a0);
+        point(cb, m1, a1);
     }
-    if (i < i1) {
-        const double4 ra = rows[i];
-        const double xa[3] = {ra.x, ra.y, ra.z};
-        double qa = 0.0, da[3];
-#pragma unroll
-        for (int d = 0; d < D; ++d) { da[d] = xa[d] - z[d]; qa = fma(da[d], da[d], qa); }
-        const double wa = ra.w * exp(c * qa);
-        m0 += wa;
-#pragma unroll
-        for (int d = 0; d < D; ++d) a0[d] = fma(wa, da[d], a0[d]);
-    }
+    if (i < i1) point(ra, m0, a0);
     m = m0 + m1;
 #pragma unroll
     for (int d = 0; d < 3; ++d) gacc[d] = (d < D) ? a0[d] + a1[d] : 0.0;
@@ -195,6 +191,7 @@ struct SqpKernel {
     // (G' has NB+1 <= 16 columns, the forward state [dx; 1] has NX+1 <= 8 rows).
     static constexpr bool kMfma = (NB + 1 <= 16) && (NX + 1 <= 8);
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
+    static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
@@ -213,7 +210,7 @@ struct SqpKernel {
             const size_t acl = (size_t)H * NX * PS;            // closed-loop A'_k (tightening scratch aliases it)
             return common + (size_t)(H + 1) * PP + (acl > tight_scratch(H) ? acl : tight_scratch(H));
         }
-        return common + (size_t)(H + 1) * NX * PS              // P'_k
+        return common + (size_t)(H + 1) * PP                   // P'_k (packed)
                + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
                + tight_scratch(H);
     }
@@ -233,7 +230,7 @@ struct SqpKernel {
             L.cd = s;
             L.Sig = s + (size_t)H * NUNC;
         } else {
-            L.P = s;   s += (size_t)(H + 1) * NX * PS;
+            L.P = s;   s += (size_t)(H + 1) * PP;
             L.W = s;   s += (size_t)NX * GS;
             L.Ms = s;  s += (size_t)GS * GS;
             L.vs = s;  s += (size_t)2 * NB + NX;
@@ -423,7 +420,8 @@ struct SqpKernel {
             if (l >= 0) {
                 double pr[PS], gc[NX];
 #pragma unroll
-                for (int m = 0; m < PS; ++m) pr[m] = Pn[l * PS + m];
+                for (int m = 0; m < NX; ++m) pr[m] = Pn[l <= m ? pidx(l, m) : pidx(m, l)];
+                pr[NX] = Pn[PO + l];
 #pragma unroll
                 for (int m = 0; m < NX; ++m) gc[m] = G[m * GS + j];
                 double acc = (j == NB) ? pr[NX] : 0.0;
@@ -468,15 +466,16 @@ struct SqpKernel {
 
     __device__ static bool riccati_factor(const Lds& L, int H, int lane, const Entries& E) {
         // P'_H = [diag(hq_H[x]) | gq_H[x]]
-        double* PH = L.P + (size_t)H * NX * PS;
+        double* PH = L.P + (size_t)H * PP;
         for (int e = lane; e < NX * PS; e += 64) {
             const int i = e / PS, j = e % PS;
-            PH[e] = (j == NX) ? L.gq[H * NB + i] : ((i == j) ? L.hq[H * NB + i] : 0.0);
+            if (j == NX) PH[PO + i] = L.gq[H * NB + i];
+            else if (i <= j) PH[pidx(i, j)] = (i == j) ? L.hq[H * NB + i] : 0.0;
         }
         WSYNC();
         bool ok = true;
         for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * NX * PS;
+            const double* Pn = L.P + (size_t)(k + 1) * PP;
             const double* G = L.G + (size_t)k * NX * GS;
             phase_W(L, Pn, G, E);
             WSYNC();
@@ -484,7 +483,7 @@ struct SqpKernel {
             WSYNC();
             double Ri[NU][NU];
             ok = load_Ri(L, Ri) && ok;
-            double* Pk = L.P + (size_t)k * NX * PS;
+            double* Pk = L.P + (size_t)k * PP;
             double* Kk = L.K + (size_t)k * NU * PS;
 #pragma unroll
             for (int r = 0; r < R3; ++r) {
@@ -508,8 +507,7 @@ struct SqpKernel {
                     double acc = L.Ms[i * GS + j];
 #pragma unroll
                     for (int a = 0; a < NU; ++a) acc = fma(-mi[a], tr[a], acc);
-                    Pk[i * PS + jj] = acc;
-                    if (j < NX && j != i) Pk[j * PS + i] = acc;
+                    Pk[jj == NX ? PO + i : pidx(i, j)] = acc;   // entries decode with i <= j
                 } else {
                     double t = 0.0;
 #pragma unroll
@@ -532,16 +530,17 @@ struct SqpKernel {
 
     // Vector-only backward sweep with the stored factorisation (Mehrotra corrector): p, kff.
     __device__ static void riccati_vector(const Lds& L, int H, int lane) {
-        if (lane < NX) L.P[(size_t)H * NX * PS + lane * PS + NX] = L.gq[H * NB + lane];
+        if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
         WSYNC();
         for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * NX * PS;
+            const double* Pn = L.P + (size_t)(k + 1) * PP;
             const double* G = L.G + (size_t)k * NX * GS;
             double* pv = L.vs;
             if (lane < NX) {
                 double pr[PS], c[NX];
 #pragma unroll
-                for (int m = 0; m < PS; ++m) pr[m] = Pn[lane * PS + m];
+                for (int m = 0; m < NX; ++m) pr[m] = Pn[lane <= m ? pidx(lane, m) : pidx(m, lane)];
+                pr[NX] = Pn[PO + lane];
 #pragma unroll
                 for (int m = 0; m < NX; ++m) c[m] = G[m * GS + NB];
                 double acc = pr[NX];
@@ -579,7 +578,7 @@ struct SqpKernel {
                         for (int l = 0; l < NX; ++l) acc = fma(gcol[l], pvl[l], acc);
 #pragma unroll
                         for (int a = 0; a < NU; ++a) acc = fma(kc[a], gu[a], acc);
-                        L.P[(size_t)k * NX * PS + i * PS + NX] = acc;
+                        L.P[(size_t)k * PP + PO + i] = acc;
                     }
                 } else {
                     const int a = lane - NX;
@@ -651,12 +650,13 @@ struct SqpKernel {
             for (int j = 0; j < NX; ++j) du = fma(kr[j], dx[j], du);
             dd[NX + a] = (lane < H) ? du : 0.0;
         }
-        const double* Pn = L.P + (size_t)(kk + 1) * NX * PS;
+        const double* Pn = L.P + (size_t)(kk + 1) * PP;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             double pr[PS];
 #pragma unroll
-            for (int j = 0; j < PS; ++j) pr[j] = Pn[i * PS + j];
+            for (int j = 0; j < NX; ++j) pr[j] = Pn[i <= j ? pidx(i, j) : pidx(j, i)];
+            pr[NX] = Pn[PO + i];
             double acc = pr[NX];
 #pragma unroll
             for (int j = 0; j < NX; ++j) acc = fma(pr[j], dxn[j], acc);
@@ -923,7 +923,6 @@ struct SqpKernel {
     // readlane broadcast); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
     __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
-        constexpr int PO = NX * (NX + 1) / 2;
         double* T = L.hq;
         double* VT = L.dxv;
         for (int e = lane; e < H * NX; e += 64) {
@@ -1072,7 +1071,8 @@ struct SqpKernel {
         }
     }
 
-    __device__ static double max_step(double v, double dv) { return dv < 0.0 ? -v / dv : 1e300; }
+    // largest alpha with v + alpha dv >= 0 (v > 0); reciprocal instead of an IEEE division sequence
+    __device__ static double max_step(double v, double dv) { return dv < 0.0 ? v * fast_rcp(-dv) : 1e300; }
 
     // cost Hessian diagonal of stage variable v on lane k (acados cost_scaling: dt on stages, 1 terminal)
     __device__ static double hdiag(const ProblemDev& P, int v, int lane, int H) {
@@ -1254,8 +1254,8 @@ struct SqpKernel {
                 d[v] = (lane == 0 && v < NX) ? x0[v] - w[v] : 0.0;   // dx_0 = e0 fixed
                 sl[v] = av ? fmax(w[v] - lbv(v), 1e-2) : 1.0;
                 su[v] = av ? fmax(ubv(v) - w[v], 1e-2) : 1.0;
-                ll[v] = av ? P.qp_mu0 / sl[v] : 0.0;
-                lu[v] = av ? P.qp_mu0 / su[v] : 0.0;
+                ll[v] = av ? P.qp_mu0 * fast_rcp(sl[v]) : 0.0;
+                lu[v] = av ? P.qp_mu0 * fast_rcp(su[v]) : 0.0;
             }
 #pragma unroll
             for (int i = 0; i < NX; ++i) piq[i] = 0.0;
@@ -1281,8 +1281,9 @@ struct SqpKernel {
                         mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
                         if (on) {
                             // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
-                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] / sl[v] + lu[v] / su[v] : 0.0);
-                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl / sl[v] - lu[v] - lu[v] * ru / su[v] : 0.0;
+                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
+                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] * isl + lu[v] * isu : 0.0);
+                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl * isl - lu[v] - lu[v] * ru * isu : 0.0;
                         }
                     }
 #pragma unroll
@@ -1327,8 +1328,8 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
-                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
+                            const double dll = -ll[v] - ll[v] * dsl * fast_rcp(sl[v]);
+                            const double dlu = -lu[v] - lu[v] * dsu * fast_rcp(su[v]);
                             amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl), max_step(su[v], dsu)),
                                                    fmin(max_step(ll[v], dll), max_step(lu[v], dlu))));
                         }
@@ -1341,8 +1342,8 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
-                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
+                            const double dll = -ll[v] - ll[v] * dsl * fast_rcp(sl[v]);
+                            const double dlu = -lu[v] - lu[v] * dsu * fast_rcp(su[v]);
                             mua_l += (ll[v] + a_aff * dll) * (sl[v] + a_aff * dsl) + (lu[v] + a_aff * dlu) * (su[v] + a_aff * dsu);
                         }
                     }
@@ -1359,9 +1360,10 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] - ll[v] * dsl / sl[v];
-                            const double dlu = -lu[v] - lu[v] * dsu / su[v];
-                            L.gq[k * NB + v] += (dll * dsl - smu) / sl[v] - (dlu * dsu - smu) / su[v];
+                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
+                            const double dll = -ll[v] - ll[v] * dsl * isl;
+                            const double dlu = -lu[v] - lu[v] * dsu * isu;
+                            L.gq[k * NB + v] += (dll * dsl - smu) * isl - (dlu * dsu - smu) * isu;
                         }
                     }
                     WSYNC();
@@ -1394,14 +1396,15 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsla = dda[v] + rl, dsua = -dda[v] + ru;
-                            const double dlla = -ll[v] - ll[v] * dsla / sl[v];
-                            const double dlua = -lu[v] - lu[v] * dsua / su[v];
+                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
+                            const double dlla = -ll[v] - ll[v] * dsla * isl;
+                            const double dlua = -lu[v] - lu[v] * dsua * isu;
                             const double rml = ll[v] * sl[v] + dlla * dsla - smu;
                             const double rmu = lu[v] * su[v] + dlua * dsua - smu;
                             dsl[v] = dd[v] + rl;
                             dsu[v] = -dd[v] + ru;
-                            dll[v] = (-rml - ll[v] * dsl[v]) / sl[v];
-                            dlu[v] = (-rmu - lu[v] * dsu[v]) / su[v];
+                            dll[v] = (-rml - ll[v] * dsl[v]) * isl;
+                            dlu[v] = (-rmu - lu[v] * dsu[v]) * isu;
                             amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
                                                    fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
                         }

@@ -21,6 +21,36 @@ def oracle_gps(data, hyp):
     return [O.ExactGP(X, y, *hyp[i]) for i, (X, y) in enumerate(data)]
 
 
+def fitc_weights(gpp, M, seed=1337):
+    """FITC (S, w) per GP from the product's restatement of `gpmpc/gpmpc.py:377-400` (pinned by
+    tests/test_cpu_host.py::test_fitc_weights_match_reference_fixture)."""
+    from gpmpc.gpmpc import GPMPC
+
+    for gp in gpp:
+        gp.K, gp.K_inv = gp.compute_covariances()
+    me = type("Me", (), {})()
+    me.gaussian_process = gpp
+    me.np_random = np.random.default_rng(seed)
+    return GPMPC.precompute_sparse_posterior_mean(me, M)
+
+
+def fitc_oracle_gps(gpo, fitc):
+    """Oracle GPs whose mean is the FITC approximation k(z, S) w; the variance stays exact."""
+    for gp, (S, w) in zip(gpo, fitc):
+        S = np.asarray(S, dtype=np.float64).reshape(len(w), -1)
+        w = np.asarray(w, dtype=np.float64)
+
+        def mean(Z, gp=gp, S=S, w=w):
+            return O.se_kernel(np.atleast_2d(Z), S, gp.ell, gp.sf2) @ w
+
+        def mean_grad(z, gp=gp, S=S, w=w):
+            wv = O.se_kernel(z[None, :], S, gp.ell, gp.sf2)[0] * w
+            return wv.sum(), (wv[:, None] * (S - z[None, :])).sum(0) / gp.ell**2
+
+        gp.mean, gp.mean_grad = mean, mean_grad
+    return gpo
+
+
 def product_gps(data, hyp, device="cpu"):
     import torch
 
@@ -58,4 +88,5 @@ def oracle_step(spec, sol: O.SQPSolver, gps, x0, step, H, traj, prev, prob=0.95,
     return st, sc, ic
 
 
-__all__ = ["problem", "oracle_gps", "product_gps", "lqr", "oracle_step", "initial_states", "O"]
+__all__ = ["problem", "oracle_gps", "product_gps", "fitc_weights", "fitc_oracle_gps", "lqr", "oracle_step",
+           "initial_states", "O"]

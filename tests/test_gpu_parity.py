@@ -11,7 +11,8 @@ Tolerances (float64 everywhere):
 import numpy as np
 import pytest
 
-from helpers import O, initial_states, lqr, oracle_gps, oracle_step, problem, product_gps
+from helpers import (O, fitc_oracle_gps, fitc_weights, initial_states, lqr, oracle_gps, oracle_step, problem,
+                     product_gps)
 
 pytestmark = pytest.mark.gpu
 
@@ -60,19 +61,24 @@ def test_gp_predict_edge_cases():
     assert abs(float(m[0])) < 1e-12 and abs(float(v[0]) - hyp[1][1]) < 1e-12
 
 
-@pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 4, 3), ("cartpole", 50, 20, 3, 3),
-                                               ("quad3d", 60, 15, 2, 2)])
-def test_closed_loop_parity(name, N, H, B, steps):
+@pytest.mark.parametrize("name,N,H,B,steps,M", [("quad2d", 200, 30, 4, 3, None), ("cartpole", 50, 20, 3, 3, None),
+                                                 ("quad3d", 60, 15, 2, 2, None), ("quad3d", 120, 40, 1, 2, 60),
+                                                 ("quad2d", 1000, 30, 2, 2, None)])
+def test_closed_loop_parity(name, N, H, B, steps, M):
+    """M: FITC mean on M inducing rows (`gpmpc/gpmpc.py:377-400`, config 5's sparse GP), exact variance."""
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
     spec, data, hyp = problem(name, N)
     gpo = oracle_gps(data, hyp)
     gpp = product_gps(data, hyp)
+    fitc = fitc_weights(gpp, M) if M else None
+    if fitc is not None:
+        gpo = fitc_oracle_gps(gpo, fitc)
     mats = lqr(spec)
     tol = 1e-9
     solver = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)  # tight KKT for parity
-    solver.set_gps(gpp)
+    solver.set_gps(gpp, fitc=fitc)
     solver.set_tightening(True, 0.95, *mats)
     solver.reset(reset_iterate=True)
     sd = spec.to_dict()
@@ -136,3 +142,55 @@ def test_plant_step_matches_oracle():
         for b in range(7):
             np.testing.assert_allclose(xn[b], dyn.rk4(x[b], u[b])[0], rtol=1e-13, atol=1e-13)
         assert (ts.cpu().numpy() == 1).all()
+
+
+def test_nominal_mpc_class_matches_oracle():
+    """`gpmpc/mpc.py` MPC: prior model only, no tightening, uh = +1e-8, default acados tolerances.
+    Compared at the converged solution within the north-star tolerance (1e-4 relative)."""
+    torch = _torch()
+    from gpmpc.mpc import MPC
+
+    spec, _, _ = problem("cartpole", 10)
+    H = 10
+    ctrl = MPC("cartpole", horizon=H)
+    ctrl.reset()
+    sd = spec.to_dict()
+    orc = O.SQPSolver(sd, O.Dynamics(sd, None), H, O.SQPOptions(qp_tol=1e-10, qp_max_iter=100))
+    plant = O.Dynamics(sd, None, params=spec.true_params)
+    traj = spec.reference_trajectory()
+    x = initial_states(spec, traj, 1)[0][0]
+    for step in range(3):
+        u = ctrl.select_action(x)
+        st, _, _ = oracle_step(spec, orc, None, x, step, H, traj, None, tighten=False, uh=1e-8)
+        assert st == 0
+        xs, us, _ = (a.cpu().numpy()[0] for a in ctrl.solver.solution())
+        assert np.abs(xs - orc.x).max() <= 1e-4 * (1 + np.abs(orc.x).max())
+        assert np.abs(u - orc.u[0]).max() <= 1e-4 * (1 + np.abs(orc.u).max())
+        x = plant.rk4(x, u)[0]
+
+
+def test_gpmpc_class_select_action_matches_oracle():
+    """The drop-in `GPMPC.select_action` (B=1, numpy in/out) over a short closed loop."""
+    torch = _torch()
+    from gpmpc.gpmpc import GPMPC
+
+    spec, data, hyp = problem("quad2d", 120)
+    H = 12
+    ctrl = GPMPC("quad2d", horizon=H, prob=0.95)
+    ctrl.set_gaussian_processes(product_gps(data, hyp))
+    ctrl.reset()
+    gpo = oracle_gps(data, hyp)
+    sd = spec.to_dict()
+    orc = O.SQPSolver(sd, O.Dynamics(sd, gpo), H, O.SQPOptions(qp_tol=1e-10, qp_max_iter=100))
+    plant = O.Dynamics(sd, None, params=spec.true_params)
+    traj = spec.reference_trajectory()
+    x = initial_states(spec, traj, 1)[0][0]
+    mats = lqr(spec)
+    prev = None
+    for step in range(3):
+        u = ctrl.select_action(x)
+        st, _, _ = oracle_step(spec, orc, gpo, x, step, H, traj, prev, lqr_mats=mats)
+        assert st == 0
+        assert np.abs(u - orc.u[0]).max() <= 1e-4 * (1 + np.abs(orc.u).max()), (step, u, orc.u[0])
+        prev = (orc.x.T.copy(), orc.u.T.copy())
+        x = plant.rk4(x, u)[0]

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--no-gp", action="store_true", help="nominal dynamics (isolates the GP sums)")
     args = ap.parse_args()
     from gpmpc import _lib
     from gpmpc.gp import GaussianProcess
@@ -50,8 +51,11 @@ def main():
     dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
     mats = setup_prior_dynamics(dfdx, dfdu, np.diag(spec.q_diag), np.diag(spec.r_diag), spec.dt)
     s = BatchSolver(spec, H, B)
-    s.set_gps(gps)
-    s.set_tightening(True, 0.95, *mats)
+    if args.no_gp:
+        s.set_gps(None)
+    else:
+        s.set_gps(gps)
+        s.set_tightening(True, 0.95, *mats)
     s.reset(True)
     tbuf = torch.zeros(B, len(PHASES), dtype=torch.int64, device="cuda")
     _lib.check(s.lib.gpmpc_set_timing_buffer(s._h, tbuf.data_ptr()))
