@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--qp-tol", type=float, default=1e-8, help="IPM tolerance of the QP sub-problems")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
+    ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
+    ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
+                    help="tools/pmc_summary.py output of the same command (roofline.traffic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,7 +142,16 @@ def main():
     lqr_mats = setup_prior_dynamics(dfdx, dfdu, Q, R, spec.dt)
 
     solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
-    solver.set_gps(gps)
+    fitc = None
+    if args.fitc:
+        from gpmpc.gpmpc import GPMPC
+
+        for gp in gps:
+            gp.K, gp.K_inv = gp.compute_covariances()
+        me = type("Me", (), {})()
+        me.gaussian_process, me.np_random = gps, np.random.default_rng(1337)
+        fitc = GPMPC.precompute_sparse_posterior_mean(me, min(args.fitc, N))
+    solver.set_gps(gps, fitc=fitc)
     solver.set_tightening(True, 0.95, *lqr_mats)
     solver.reset(reset_iterate=True)
     traj = spec.reference_trajectory()
@@ -148,25 +160,19 @@ def main():
     x0_all, phase_all = initial_states(spec, traj, B * world, seed=1)
     obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
     tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
-    acc_sqp = torch.zeros(B, dtype=torch.int64, device=dev)
-    acc_qp = torch.zeros(B, dtype=torch.int64, device=dev)
-    acc_st = torch.zeros(5, dtype=torch.int64, device=dev)
-    codes = torch.arange(5, device=dev, dtype=torch.int32)
+    stats_buf = torch.zeros(B, 8, dtype=torch.int64, device=dev)   # accumulated inside the SQP kernel
+    solver.set_stats(stats_buf)
 
     def step():
         u0 = solver.solve(obs, tstep)
         solver.plant_step(obs, u0, tstep, out=obs)
-        acc_sqp.add_(solver.sqp_iter)
-        acc_qp.add_(solver.qp_iter)
-        acc_st.add_((solver.status[:, None] == codes[None, :]).sum(0))
 
-    solver.set_profiling(True)   # warm-up runs the timed body exactly (events, torch kernels)
+    solver.set_profiling(True)   # warm-up runs the timed body exactly (events)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     solver.kernel_times()  # drop warm-up events
-    for t in (acc_sqp, acc_qp, acc_st):
-        t.zero_()
+    stats_buf.zero_()
     torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
@@ -181,8 +187,9 @@ def main():
     solver.set_profiling(False)
     kt = solver.kernel_times()
     stats = torch.tensor([elapsed, kt["sqp_ms"], kt["var_ms"]], dtype=torch.float64, device=dev)
-    sums = torch.stack([acc_sqp.sum(), acc_qp.sum()]).to(torch.float64)
-    status_counts = acc_st.to(torch.float64)
+    tot = stats_buf.sum(0).to(torch.float64)
+    sums = tot[:2].clone()
+    status_counts = tot[2:7].clone()
     if dist is not None:
         dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
@@ -201,6 +208,17 @@ def main():
         achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
         var_ms = float(stats[2]) / max(kt["var_launches"], 1)
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if kt["var_launches"] else None
+        workload = f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}, " \
+                   f"{B} instances per GPU, closed loop"
+        traffic = None
+        try:
+            with open(args.pmc_summary) as fh:
+                pmc = json.load(fh)
+            if pmc.get("config", {}).get("workload") == workload:
+                e = pmc["kernels"].get("gpmpc::sqp_step_kernel<%d>" % spec.model_id, {})
+                traffic = e.get("hbm_bytes_est")
+        except (OSError, ValueError, KeyError):
+            traffic = None
         cpu = None
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats)
@@ -217,12 +235,12 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded GP training set, initial states, figure-eight reference)",
-            "config": {"workload": f"{spec.name} GP-MPC N={N} H={H}, {B} instances per GPU, closed loop",
+            "config": {"workload": workload,
                        "model": spec.name, "global_batch": total_instances, "horizon": H, "n_train": N,
                        "parallelism": f"instances sharded over {world} GPU(s), GP replicated"},
             "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "traffic": None,
+                         "traffic": traffic,
                          "note": "FP64 GP mean+gradient contraction flops / HIP-event kernel time; peak = FP64 "
                                  "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
                                  "Riccati recursion"},

@@ -75,6 +75,7 @@ struct gpmpc_handle {
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_var, ev_sqp;
     unsigned long long* timing = nullptr;  // diagnostic phase cycles (GPMPC_TIMING builds)
+    long long* stats = nullptr;            // optional per-instance solver statistics accumulators
     int32_t* scratch_i = nullptr;   // [2][max_batch]
     double* scratch_d = nullptr;    // [max_batch][4]
 };
@@ -416,7 +417,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     }
     // 2. the SQP step
     StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight};
-    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing};
+    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing, h->stats};
     // optional outputs go to handle-owned scratch when NULL
     if (!io.sqp_iter) io.sqp_iter = h->scratch_i;
     if (!io.qp_iter) io.qp_iter = h->scratch_i + h->max_batch;
@@ -468,6 +469,12 @@ gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var,
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     h->timing = (unsigned long long*)timing_dev;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    h->stats = (long long*)stats_dev;
     return GPMPC_OK;
 }
 

@@ -77,7 +77,8 @@ struct StepIO {
     int32_t* sqp_iter;       // [B] out
     int32_t* qp_iter;        // [B] out, total IPM iterations
     double* res;             // [B][4] out, final NLP residuals (stat, eq, ineq, comp)
-    unsigned long long* timing;  // [B][8] phase cycles (GPMPC_TIMING builds only), may be null
+    unsigned long long* timing;  // [B][kPhases] phase cycles (GPMPC_TIMING builds only), may be null
+    long long* stats;            // [B][8] running sums: sqp iters, qp iters, status 0..4 counts; may be null
 };
 
 // Arguments of the GP posterior kernel (gp_kernels.hip).

@@ -1481,6 +1481,12 @@ struct SqpKernel {
 #pragma unroll
             for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
             S.has_prev[b] = 1;
+            if (io.stats != nullptr) {
+                long long* st = io.stats + (size_t)b * 8;
+                st[0] += it;
+                st[1] += qp_total;
+                if (status >= 0 && status <= 4) st[2 + status] += 1;
+            }
         }
     }
 };

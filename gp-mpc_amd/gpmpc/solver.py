@@ -142,6 +142,13 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_tightening(self._h, 1, inverse_cdf(prob, self.nx), Ad.ctypes.data,
                                                  Bd.ctypes.data, K.ctypes.data))
 
+    def set_stats(self, buf: torch.Tensor | None):
+        """Device int64 (B, 8) accumulator of SQP/QP iterations and status counts (or None)."""
+        if buf is not None:
+            assert buf.shape == (self.batch, 8) and buf.dtype == torch.int64 and buf.device == self.device
+        self._stats = buf
+        _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr()))
+
     def set_profiling(self, enabled: bool):
         _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))
 

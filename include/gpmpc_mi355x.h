@@ -146,6 +146,12 @@ gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var,
  * per-phase shader-clock cycles of each instance's last solve; NULL disables. */
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
 
+/* Optional device buffer [max_batch][8] (int64) of running solver statistics, accumulated by the
+ * SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
+ * of solves that ended with status s (0..4).  The caller zeroes it; NULL disables (default).
+ * Replaces reading acados' per-solve "sqp_iter" / "qp_iter" / status stats in a host loop. */
+gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev);
+
 /* LDS bytes one instance's workgroup needs (capacity planning / tests). */
 int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon);
 
