@@ -196,9 +196,10 @@ def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: st
         loss = -exact_mll(gp)
         loss.backward()
         optim.step()
-        if abs(last - float(loss)) < 1e-3:
+        lv = float(loss.detach())
+        if abs(last - lv) < 1e-3:
             break
-        last = float(loss)
+        last = lv
     for p in params:
         p.requires_grad_(False)
     gp._dev = None

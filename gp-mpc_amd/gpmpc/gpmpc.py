@@ -91,9 +91,15 @@ class GPMPC:
         x_train = torch.tensor(np.asarray(x, dtype=np.float64))
         y_train = torch.tensor(np.asarray(y, dtype=np.float64))
         gps = []
+        from . import distributed as D
+
+        _, size = D.world()
         for i, idx in enumerate(self.gp_idx):
             gp = GaussianProcess(x_train[:, idx], y_train[:, i])
-            fit_gp(gp, n_train=iterations, lr=lr, device="cpu")
+            if size > 1:   # data-parallel fit: one all-reduce of the MLL gradient per Adam step
+                D.fit_gp_allreduce(gp, n_train=iterations, lr=lr)
+            else:
+                fit_gp(gp, n_train=iterations, lr=lr, device="cpu")
             gps.append(gp)
         self.set_gaussian_processes(gps)
 

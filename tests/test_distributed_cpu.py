@@ -66,3 +66,49 @@ def test_two_rank_sharding_and_replication():
 
     ref = make_training_data(get_spec("quad2d"), 16, seed=1)
     np.testing.assert_array_equal(np.array(x0[0]), ref[0][0])
+
+
+def _fit_worker(rank, world, port, out):
+    sys.path[:0] = [str(ROOT / "gp-mpc_amd"), str(ROOT)]
+    import torch
+    import torch.distributed as dist
+
+    from gpmpc import distributed as D
+    from gpmpc.gp import GaussianProcess
+    from gpmpc.models import get_spec
+    from gpmpc.synthetic import make_training_data
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, y = make_training_data(get_spec("quad2d"), 60, seed=1)[1]
+    gp = GaussianProcess(torch.tensor(X), torch.tensor(y))
+    it = D.fit_gp_allreduce(gp, n_train=40, lr=0.05)
+    out.put((rank, it, gp.lengthscale, gp.outputscale, gp.noise))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gp_fit_allreduce_matches_single_process():
+    """row-split MLL gradient + all-reduce == the single-process autograd fit."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fit_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1:] == res[1][1:]            # replicas bit-identical without a broadcast
+    sys.path[:0] = [str(ROOT / "gp-mpc_amd")]
+    import torch
+
+    from gpmpc.gp import GaussianProcess, fit_gp
+    from gpmpc.models import get_spec
+    from gpmpc.synthetic import make_training_data
+
+    X, y = make_training_data(get_spec("quad2d"), 60, seed=1)[1]
+    ref = GaussianProcess(torch.tensor(X), torch.tensor(y))
+    fit_gp(ref, n_train=40, lr=0.05)
+    np.testing.assert_allclose(res[0][2:], [ref.lengthscale, ref.outputscale, ref.noise], rtol=1e-8)
