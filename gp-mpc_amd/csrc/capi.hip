@@ -69,6 +69,7 @@ struct gpmpc_handle {
     double* gp_rows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
     double* gp_vrows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
     double* gp_linvT[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
+    double* gp_tiles[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};   // tX | tW (MFMA tile pack)
     int gp_npad[kMaxGP] = {0, 0, 0, 0};
     // optional per-kernel HIP-event timing (bench.py's roofline leg)
     bool profiling = false;
@@ -106,6 +107,7 @@ static void free_handle(gpmpc_handle* h) {
         if (h->gp_rows[g]) (void)hipFree(h->gp_rows[g]);
         if (h->gp_vrows[g]) (void)hipFree(h->gp_vrows[g]);
         if (h->gp_linvT[g]) (void)hipFree(h->gp_linvT[g]);
+        if (h->gp_tiles[g]) (void)hipFree(h->gp_tiles[g]);
     }
     delete h;
 }
@@ -275,12 +277,37 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
     const bool exact = (Xv == X);
     if (!exact) pack(Xv, nullptr, nv, vrows);
     const int npad = (nv + 15) / 16 * 16;
-    for (double** p : {&h->gp_rows[gp_id], &h->gp_vrows[gp_id], &h->gp_linvT[gp_id]}) {
+    // MFMA tile pack of the mean rows, centred on their mean (sqp_kernel.hip gp_tiles)
+    const double c = -0.5 / (lengthscale * lengthscale);
+    double xbar[3] = {0.0, 0.0, 0.0};
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < d; ++k) xbar[k] += X[(size_t)i * d + k] / n;
+    const int ntile = (n + 15) / 16;
+    std::vector<double> tiles((size_t)ntile * (64 + 64), 0.0);
+    double* tX = tiles.data();
+    double* tW = tiles.data() + (size_t)ntile * 64;
+    const double m2c = 1.0 / (lengthscale * lengthscale);
+    for (int i = 0; i < n; ++i) {
+        // MFMA C/D rows: register q of lane group grp holds row grp + 4q
+        const int t = i / 16, r = i % 16, grp = r % 4, q = r / 4;
+        double xc[3] = {0.0, 0.0, 0.0}, sq = 0.0;
+        for (int k = 0; k < d; ++k) {
+            xc[k] = X[(size_t)i * d + k] - xbar[k];
+            sq += xc[k] * xc[k];
+            tX[(size_t)t * 64 + r * 4 + k] = m2c * xc[k];
+        }
+        tX[(size_t)t * 64 + r * 4 + 3] = c * sq;
+        const double wv[4] = {alpha[i], alpha[i] * xc[0], alpha[i] * xc[1], alpha[i] * xc[2]};
+        for (int j = 0; j < 4; ++j) tW[(size_t)t * 64 + (grp * 4 + j) * 4 + q] = wv[j];
+    }
+    for (double** p : {&h->gp_rows[gp_id], &h->gp_vrows[gp_id], &h->gp_linvT[gp_id], &h->gp_tiles[gp_id]}) {
         if (*p) HIPCHK(hipFree(*p));
         *p = nullptr;
     }
     HIPCHK(hipMalloc(&h->gp_rows[gp_id], rows.size() * sizeof(double)));
     HIPCHK(hipMemcpy(h->gp_rows[gp_id], rows.data(), rows.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&h->gp_tiles[gp_id], tiles.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(h->gp_tiles[gp_id], tiles.data(), tiles.size() * sizeof(double), hipMemcpyHostToDevice));
     if (!exact) {
         HIPCHK(hipMalloc(&h->gp_vrows[gp_id], vrows.size() * sizeof(double)));
         HIPCHK(hipMemcpy(h->gp_vrows[gp_id], vrows.data(), vrows.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -296,6 +323,10 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
     g.rows = h->gp_rows[gp_id];
     g.vrows = exact ? h->gp_rows[gp_id] : h->gp_vrows[gp_id];
     g.linvT = h->gp_linvT[gp_id];
+    g.tX = h->gp_tiles[gp_id];
+    g.tW = h->gp_tiles[gp_id] + (size_t)ntile * 64;
+    g.ntile = ntile;
+    for (int k = 0; k < 3; ++k) g.xbar[k] = xbar[k];
     g.n = n;
     g.nv = nv;
     g.d = d;
@@ -526,6 +557,17 @@ gpmpc_status gpmpc_gp_predict(gpmpc_handle* h, int32_t gp_id, const double* Z, i
     return GPMPC_OK;
 }
 
+gpmpc_status gpmpc_gp_mean_grad(gpmpc_handle* h, int32_t gp_id, const double* Z, int32_t P, double* mean,
+                                double* grad, void* stream) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (gp_id < 0 || gp_id >= h->md.ngp || !h->gp_set[gp_id]) return fail(GPMPC_ERR_STATE, "GP not set");
+    if (P < 0 || (P > 0 && !Z)) return fail(GPMPC_ERR_ARG, "bad points");
+    if (P == 0) return GPMPC_OK;
+    (void)hipSetDevice(h->device);
+    HIPCHK(launch_gp_mean_grad(h->P.gp[gp_id], Z, P, mean, grad, (hipStream_t)stream));
+    return GPMPC_OK;
+}
+
 gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double* rows, const double* linvT,
                                 double lengthscale, double outputscale, double noise, const double* Z, int32_t P,
                                 double* mean, double* var, int32_t with_noise, void* stream) {
@@ -535,7 +577,15 @@ gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double
     if (var && !linvT) return fail(GPMPC_ERR_ARG, "variance needs linvT");
     if (!(lengthscale > 0.0) || !(outputscale > 0.0) || !(noise >= 0.0)) return fail(GPMPC_ERR_ARG, "bad hyperparameters");
     if (P == 0) return GPMPC_OK;
-    GPDev g{rows, rows, linvT, n, n, d, 1.0 / (lengthscale * lengthscale), outputscale, noise};
+    GPDev g{};
+    g.rows = rows;
+    g.vrows = rows;
+    g.linvT = linvT;
+    g.n = g.nv = n;
+    g.d = d;
+    g.inv_ell2 = 1.0 / (lengthscale * lengthscale);
+    g.sf2 = outputscale;
+    g.sn2 = noise;
     PostArgs a{};
     a.Z = Z;
     a.ldz = d;

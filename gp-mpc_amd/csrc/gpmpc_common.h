@@ -24,6 +24,15 @@ struct GPDev {
                           //         (FITC: inducing inputs + posterior weights, gpmpc/gpmpc.py:377-400)
     const double* vrows;  // [nv][4]: training inputs of the variance GP (== rows for an exact GP)
     const double* linvT;  // [npad][npad] row-major (L^-1)^T, L = chol(K); NULL -> no variance
+    // MFMA tile pack of the mean rows (the SQP linearisation's GP sums, sqp_kernel.hip gp_tiles):
+    //   tX[t][16][4]     rows [(x_i - xbar)/ell^2 (zero padded to 3 dims), c|x_i - xbar|^2],
+    //                    c = -1/(2 ell^2); rows past n are zero
+    //   tW[t][4][4][4]   for lane group g and output column j: {W[i][j], i = 16t+g+4r, r = 0..3},
+    //                    W[i] = [alpha_i, alpha_i (x_i - xbar)]
+    const double* tX;
+    const double* tW;
+    int32_t ntile;
+    double xbar[3];       // centre of the mean rows (the RBF kernel is shift invariant)
     int32_t n;
     int32_t nv;
     int32_t d;
@@ -133,6 +142,7 @@ struct PostBatch {
 // Launchers (sqp_kernel.hip, gp_kernels.hip).
 hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream);
 size_t sqp_lds_bytes(int model, int H);
+hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* mean, double* grad, hipStream_t stream);
 hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream);
 hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream);
 hipError_t launch_plant(int model, const double* params, double dt, const double* x, const double* u, double* xn,

@@ -15,6 +15,8 @@
 // Lane layout: lane k (0..H) owns stage k: w_k = [x_k; u_k] (x_0 fixed to obs, u_H absent),
 // its bounds, IPM slacks/multipliers and the dynamics multiplier pi_k.  The Riccati
 // recursion is sequential over stages and parallel over matrix entries (lanes).
+#include <type_traits>
+
 #include "gpmpc_common.h"
 #include "models.h"
 
@@ -134,42 +136,103 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][
     return ok;
 }
 
-// Partial GP sums over training rows [i0, i1): m = sum alpha_i e_i, g_d = sum alpha_i e_i (x_id - z_d),
-// e_i = exp(-0.5 |z - x_i|^2 / ell^2)  (gpmpc/gp.py:12-14, 84-85; alpha = K^-1 y).
-// Rows are fetched one pair ahead so the L1/L2 latency hides under the previous pair's math.
-template <int D>
-__device__ __forceinline__ void gp_partial(const GPDev& g, const double* z, int i0, int i1, double& m, double (&gacc)[3]) {
-    const double c = -0.5 * g.inv_ell2;
-    double m0 = 0.0, m1 = 0.0;
-    double a0[3] = {0, 0, 0}, a1[3] = {0, 0, 0};
-    const double4* rows = reinterpret_cast<const double4*>(g.rows);
-    auto point = [&](const double4& r, double& msum, double (&acc)[3]) {
-        const double xr[3] = {r.x, r.y, r.z};
-        double q = 0.0, dv[3];
+// GP mean + input gradient at up to 16*NE evaluation points on v_mfma_f64_16x16x4_f64
+// (gpmpc/gp.py:12-14 covSE, :84-85 mean k(z,X) K^-1 y with alpha = K^-1 y precomputed).
+// Per 16-row training tile t (GPDev::tX / tW, centred on xbar) and 16-point evaluation tile:
+//   A  = X'_t Z'^T + c|z|^2           1 MFMA: X' rows [(x - xbar)/ell^2, c|x - xbar|^2], Z' columns
+//                                     [z - xbar, 1], C-init c|z - xbar|^2 (c = -1/(2 ell^2)), so A is
+//                                     the exponent c|z - x|^2 itself
+//   E  = exp(A)                       4 exps per lane; register r of lane l holds
+//                                     E[x = (l>>4) + 4r][z = l&15] (C/D layout), which is the
+//                                     B operand of K-step r of the next product
+//   S += W_t^T E                      4 MFMAs (K-steps r = 0..3), W = [alpha, alpha (x - xbar)]
+// so register 0 of lane (j, z) ends with S[j][z], j < 4: {sum alpha E, sum alpha (x_d - xbar_d) E}.
+// zb: [16*NE][4] {z - xbar, 1}; czz: [16*NE] c|z - xbar|^2; out: [16*NE][4].
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
+    const unsigned long long a = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    void* u = (void*)(((unsigned long long)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(u, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+template <int NE>
+__device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int nt, const double* zb,
+                                         const double* czzb, double* out, int lane) {
+    const int lr = lane >> 4, lc = lane & 15;
+    double zo[NE], czz[NE];
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            dv[d] = xr[d] - z[d];
-            q = fma(dv[d], dv[d], q);
-        }
-        const double w = r.w * exp_rbf(c * q);
-        msum += w;
-#pragma unroll
-        for (int d = 0; d < D; ++d) acc[d] = fma(w, dv[d], acc[d]);
-    };
-    const int last = max(i1 - 1, i0);
-    double4 ra = rows[min(i0, last)], rb = rows[min(i0 + 1, last)];
-    int i = i0;
-    for (; i + 1 < i1; i += 2) {
-        const double4 ca = ra, cb = rb;
-        ra = rows[min(i + 2, last)];
-        rb = rows[min(i + 3, last)];
-        point(ca, m0, a0);
-        point(cb, m1, a1);
+    for (int e = 0; e < NE; ++e) {
+        zo[e] = zb[(16 * e + lc) * 4 + lr];
+        czz[e] = czzb[16 * e + lc];
     }
-    if (i < i1) point(ra, m0, a0);
-    m = m0 + m1;
+    f64x4 acc[NE];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) gacc[d] = (d < D) ? a0[d] + a1[d] : 0.0;
+    for (int e = 0; e < NE; ++e) acc[e] = f64x4{0.0, 0.0, 0.0, 0.0};
+    // Tile operands through buffer loads (SGPR resource, per-lane byte offsets): the loads are
+    // intrinsics, so the two-tile prefetch below survives the IR optimiser (plain loads through
+    // a phi get folded back to the use), and reads past the pack return 0.
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(tX, nt * 64 * 8);
+    const __amdgpu_buffer_rsrc_t rw = make_rsrc(tW, nt * 64 * 8);
+    const int ox = (lc * 4 + lr) * 8, ow = (lr * 4 + min(lc, 3)) * 32;
+    auto ldx = [&](int t) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, ox + t * 512, 0, 0)); };
+    auto ldw = [&](int t, int h) { return __builtin_amdgcn_raw_buffer_load_b128(rw, ow + t * 512 + 16 * h, 0, 0); };
+    struct Ops { double x; decltype(ldw(0, 0)) wa, wb; };
+    auto load = [&](int t, Ops& o) { o.x = ldx(t); o.wa = ldw(t, 0); o.wb = ldw(t, 1); };
+    auto tile = [&](const Ops& o) {
+        auto d = [](unsigned lo, unsigned hi) { return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32)); };
+        const double wr[4] = {d(o.wa[0], o.wa[1]), d(o.wa[2], o.wa[3]), d(o.wb[0], o.wb[1]), d(o.wb[2], o.wb[3])};
+        f64x4 a[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) a[e] = mfma64(o.x, zo[e], f64x4{czz[e], czz[e], czz[e], czz[e]});
+        double ex[NE][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int e = 0; e < NE; ++e) ex[e][r] = exp_rbf(a[e][r]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int e = 0; e < NE; ++e) acc[e] = mfma64(wr[r], ex[e][r], acc[e]);
+    };
+    // ping-pong operand sets (no register copies on the back edge, so no wait there)
+    Ops A, B;
+    load(0, A);
+    load(1, B);
+    for (int t = 0; t < nt; t += 2) {
+        tile(A);
+        load(t + 2, A);
+        if (t + 1 < nt) tile(B);
+        load(t + 3, B);
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) out[(16 * e + lc) * 4 + lr] = acc[e][0];   // S[lr][z] (row lr = register 0)
+}
+
+template <int N, class F, int I = 0>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, F, I + 1>(static_cast<F&&>(f));
+    }
+}
+
+// One copy of the tile loop per evaluation-tile count, shared by every call site (noinline).
+// Three or four evaluation tiles (H > 32) run as two passes to bound the register footprint.
+__device__ __attribute__((noinline)) void gp_tiles_dispatch(const double* tX, const double* tW, int ntile,
+                                                          const double* zb, const double* czz, double* out,
+                                                          int lane, int ne) {
+    switch (ne) {
+        case 1: gp_tiles<1>(tX, tW, ntile, zb, czz, out, lane); break;
+        case 2: gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane); break;
+        case 3:
+            gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane);
+            gp_tiles<1>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane);
+            break;
+        default:
+            gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane);
+            gp_tiles<2>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane);
+            break;
+    }
 }
 
 template <int ID>
@@ -195,9 +258,17 @@ struct SqpKernel {
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs;
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
+    // GP evaluation scratch of the linearisation: points [NGP][16*NE][4], c|z|^2 [NGP][16*NE], sums
+    // [NGP][16*NE][4].  It aliases
+    // the P' region, which is dead between the QP solves.
+    __host__ __device__ static size_t gp_scratch(int H) { return (size_t)9 * NGP * 16 * ((H + 15) / 16); }
+    __host__ __device__ static size_t p_region(int H) {
+        const size_t pp = (size_t)(H + 1) * PP;
+        return pp > gp_scratch(H) ? pp : gp_scratch(H);
+    }
     __host__ __device__ static size_t lds_doubles(int H) {
         const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
                               + (size_t)8                    // zero slots (branch-free masked loads)
@@ -208,9 +279,9 @@ struct SqpKernel {
                               + (size_t)(H + 1) * NX;        // dx (forward sweep)
         if (kMfma) {
             const size_t acl = (size_t)H * NX * PS;            // closed-loop A'_k (tightening scratch aliases it)
-            return common + (size_t)(H + 1) * PP + (acl > tight_scratch(H) ? acl : tight_scratch(H));
+            return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H));
         }
-        return common + (size_t)(H + 1) * PP                   // P'_k (packed)
+        return common + p_region(H)                             // P'_k (packed) | GP scratch
                + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
                + tight_scratch(H);
     }
@@ -224,13 +295,16 @@ struct SqpKernel {
         L.hq = s;  s += (size_t)(H + 1) * NB;
         L.gq = s;  s += (size_t)(H + 1) * NB;
         L.dxv = s; s += (size_t)(H + 1) * NX;
+        L.gz = s;
+        L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
+        L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
         if (kMfma) {
-            L.P = s;   s += (size_t)(H + 1) * PP;
+            L.P = s;   s += p_region(H);
             L.Acl = s;
             L.cd = s;
             L.Sig = s + (size_t)H * NUNC;
         } else {
-            L.P = s;   s += (size_t)(H + 1) * PP;
+            L.P = s;   s += p_region(H);
             L.W = s;   s += (size_t)NX * GS;
             L.Ms = s;  s += (size_t)GS * GS;
             L.vs = s;  s += (size_t)2 * NB + NX;
@@ -240,30 +314,10 @@ struct SqpKernel {
         return L;
     }
 
-    // ------------------------------------------------------------------ GP sum, chunked over lanes
-    // All lanes of stage s (lanes s + c*H, c < C) hold the same point z; each sums its chunk
-    // of the training set and the partial sums are combined across the C lanes.
-    template <int G>
-    __device__ static void gp_eval(const ProblemDev& P, const double* z, int stage, int chunk, int C, int H,
-                                   double& m, double (&gg)[3]) {
-        constexpr int D = M::gp_dim[G];
-        const GPDev& g = P.gp[G];
-        const int per = (g.n + C - 1) / C;
-        const int i0 = min(g.n, chunk * per), i1 = min(g.n, i0 + per);
-        double part, gacc[3];
-        gp_partial<D>(g, z, i0, i1, part, gacc);
-        double tm = 0.0, tg[3] = {0, 0, 0};
-        for (int c = 0; c < C; ++c) {
-            const int src = stage + c * H;
-            tm += __shfl(part, src);
-#pragma unroll
-            for (int d = 0; d < D; ++d) tg[d] += __shfl(gacc[d], src);
-        }
-        m = g.sf2 * tm;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) gg[d] = (d < D) ? g.sf2 * g.inv_ell2 * tg[d] : 0.0;
-    }
-
+    // ------------------------------------------------------------------ GP sums on MFMA
+    // One pass evaluates every GP of one kind (u-only or state-dependent) at all H stage points:
+    // the stage lanes write their centred points to LDS, the whole wave runs the MFMA tile sums
+    // (gp_tiles), and every lane reads the sums of its stage back.
     template <int G>
     __device__ static void gp_input(const double* x, const double* u, double* z) {
 #pragma unroll
@@ -274,25 +328,61 @@ struct SqpKernel {
     }
 
     template <int G>
-    __device__ static void eval_gp_if(const ProblemDev& P, bool state_pass, const double* x, const double* u, int stage,
-                                      int chunk, int C, int H, double* gm, double (*gg)[3]) {
-        if (M::gp_state_dep[G] == state_pass) {
-            double z[3];
-            gp_input<G>(x, u, z);
-            gp_eval<G>(P, z, stage, chunk, C, H, gm[G], gg[G]);
-        }
+    __device__ static void gp_centred(const GPDev& g, const double* x, const double* u, double (&zc)[3]) {
+        double z[3];
+        gp_input<G>(x, u, z);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) zc[d] = d < M::gp_dim[G] ? z[d] - g.xbar[d] : 0.0;
     }
 
-    __device__ static void eval_gps(const ProblemDev& P, bool state_pass, const double* x, const double* u, int stage,
-                                    int chunk, int C, int H, double* gm, double (*gg)[3]) {
+    __device__ static void eval_gps(const ProblemDev& P, const Lds& L, bool state_pass, const double* x,
+                                    const double* u, int stage, int lane, int H, double* gm, double (*gg)[3]) {
         if (!P.use_gp) {
             if (!state_pass)
                 for (int g = 0; g < NGP; ++g) { gm[g] = 0.0; gg[g][0] = gg[g][1] = gg[g][2] = 0.0; }
             return;
         }
-        eval_gp_if<0>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
-        if constexpr (NGP > 1) eval_gp_if<1>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
-        if constexpr (NGP > 2) eval_gp_if<2>(P, state_pass, x, u, stage, chunk, C, H, gm, gg);
+        const int ne = (H + 15) >> 4, np = 16 * ne;
+        // 1. points {z - xbar, c |z - xbar|^2}; padding points are zero
+        static_for<NGP>([&](auto gi) {
+            constexpr int G = decltype(gi)::value;
+            if (M::gp_state_dep[G] != state_pass || lane >= np) return;
+            double zc[3];
+            gp_centred<G>(P.gp[G], x, u, zc);
+            const double sq = fma(zc[0], zc[0], fma(zc[1], zc[1], zc[2] * zc[2]));
+            const bool on = lane < H;
+            double* dst = L.gz + ((size_t)G * np + lane) * 4;
+            dst[0] = on ? zc[0] : 0.0;
+            dst[1] = on ? zc[1] : 0.0;
+            dst[2] = on ? zc[2] : 0.0;
+            dst[3] = 1.0;
+            L.gc[G * np + lane] = on ? -0.5 * P.gp[G].inv_ell2 * sq : 0.0;
+        });
+        WSYNC();
+        // 2. MFMA tile sums
+        static_for<NGP>([&](auto gi) {
+            constexpr int G = decltype(gi)::value;
+            if (M::gp_state_dep[G] != state_pass) return;
+            const GPDev& g = P.gp[G];
+            gp_tiles_dispatch(g.tX, g.tW, g.ntile, L.gz + (size_t)G * np * 4, L.gc + G * np, L.gs + (size_t)G * np * 4,
+                              lane, ne);
+        });
+        WSYNC();
+        // 3. mean sf2 S0 and input gradient sf2/ell^2 (S_{1+d} - (z_d - xbar_d) S0) of this lane's stage
+        static_for<NGP>([&](auto gi) {
+            constexpr int G = decltype(gi)::value;
+            if (M::gp_state_dep[G] != state_pass) return;
+            const GPDev& g = P.gp[G];
+            const double* o = L.gs + ((size_t)G * np + stage) * 4;
+            const double s0 = o[0], s1 = o[1], s2 = o[2], s3 = o[3];
+            double zc[3];
+            gp_centred<G>(g, x, u, zc);
+            const double gs = g.sf2 * g.inv_ell2;
+            gm[G] = g.sf2 * s0;
+            gg[G][0] = gs * fma(-zc[0], s0, s1);
+            gg[G][1] = M::gp_dim[G] > 1 ? gs * fma(-zc[1], s0, s2) : 0.0;
+            gg[G][2] = M::gp_dim[G] > 2 ? gs * fma(-zc[2], s0, s3) : 0.0;
+        });
     }
 
     // ------------------------------------------------------------------ linearisation
@@ -313,7 +403,7 @@ struct SqpKernel {
         const double h = P.dt;
         double xs[4][NX], gm[4][NGP], gg[4][NGP][3];
         double gm0[NGP], gg0[NGP][3];
-        eval_gps(P, false, x, u, stage, chunk, C, H, gm0, gg0);  // GPs of u only: once per stage
+        eval_gps(P, L, false, x, u, stage, lane, H, gm0, gg0);  // GPs of u only: once per stage
         double kprev[NX], acc[NX];
         const double cs[4] = {0.0, 0.5, 0.5, 1.0}, ws[4] = {1.0, 2.0, 2.0, 1.0};
 #pragma unroll
@@ -325,7 +415,7 @@ struct SqpKernel {
                 gm[s][g] = gm0[g];
                 gg[s][g][0] = gg0[g][0]; gg[s][g][1] = gg0[g][1]; gg[s][g][2] = gg0[g][2];
             }
-            eval_gps(P, true, xs[s], u, stage, chunk, C, H, gm[s], gg[s]);
+            eval_gps(P, L, true, xs[s], u, stage, lane, H, gm[s], gg[s]);
             M::f(P.params, xs[s], u, gm[s], kprev);
 #pragma unroll
             for (int i = 0; i < NX; ++i) acc[i] = (s == 0) ? kprev[i] : fma(ws[s], kprev[i], acc[i]);
@@ -1494,6 +1584,35 @@ struct SqpKernel {
 }  // namespace gpmpc
 
 namespace gpmpc {
+
+// GP mean + input gradient of the linearisation (gp_tiles) for arbitrary points: one wavefront
+// per 64 points.  Z [P][d] -> mean [P] = sf2 S0, grad [P][d] = sf2/ell^2 (S_{1+k} - (z_k - xbar_k) S0).
+__global__ __launch_bounds__(64) void gp_mean_grad_kernel(GPDev g, const double* Z, int P, double* mean, double* grad) {
+    __shared__ double zb[64 * 4], czz[64], out[64 * 4];
+    const int lane = threadIdx.x, p = blockIdx.x * 64 + lane;
+    double zc[3] = {0.0, 0.0, 0.0};
+    if (p < P)
+        for (int k = 0; k < g.d; ++k) zc[k] = Z[(size_t)p * g.d + k] - g.xbar[k];
+    zb[lane * 4 + 0] = zc[0];
+    zb[lane * 4 + 1] = zc[1];
+    zb[lane * 4 + 2] = zc[2];
+    zb[lane * 4 + 3] = 1.0;
+    czz[lane] = -0.5 * g.inv_ell2 * fma(zc[0], zc[0], fma(zc[1], zc[1], zc[2] * zc[2]));
+    __syncthreads();
+    gp_tiles_dispatch(g.tX, g.tW, g.ntile, zb, czz, out, lane, 4);
+    __syncthreads();
+    if (p < P) {
+        const double s0 = out[lane * 4];
+        if (mean) mean[p] = g.sf2 * s0;
+        if (grad)
+            for (int k = 0; k < g.d; ++k) grad[(size_t)p * g.d + k] = g.sf2 * g.inv_ell2 * fma(-zc[k], s0, out[lane * 4 + 1 + k]);
+    }
+}
+
+hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* mean, double* grad, hipStream_t stream) {
+    hipLaunchKernelGGL(gp_mean_grad_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, g, Z, P, mean, grad);
+    return hipGetLastError();
+}
 
 template <int ID>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {

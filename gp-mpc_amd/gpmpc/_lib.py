@@ -38,6 +38,7 @@ SIGNATURES = {
     "gpmpc_solve": (_I, [_P, _I, _P, _P, _P, _P, _P, _P, _P, _P]),
     "gpmpc_get_solution": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpmpc_gp_predict": (_I, [_P, _I, _P, _I, _P, _P, _I, _P]),
+    "gpmpc_gp_mean_grad": (_I, [_P, _I, _P, _I, _P, _P, _P]),
     "gpmpc_gp_posterior": (_I, [_I, _I, _I, _P, _P, _D, _D, _D, _P, _I, _P, _P, _I, _P]),
     "gpmpc_plant_step": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
     "gpmpc_set_profiling": (_I, [_P, _I]),

@@ -133,6 +133,17 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_use_gp(self._h, 1))
         self.gps = gps
 
+    def gp_mean_grad(self, gp_id: int, z: torch.Tensor):
+        """GP mean (P,) and input gradient (P, d) at z (P, d) through the linearisation's MFMA tile
+        sums (the casadi mean + AD of `gpmpc/gp.py:72-85`, `gpmpc/gpmpc.py:189-209`)."""
+        z = z.to(self.device, torch.float64).contiguous()
+        P = z.shape[0]
+        mean = torch.empty(P, dtype=torch.float64, device=self.device)
+        grad = torch.empty(P, z.shape[1], dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.gpmpc_gp_mean_grad(self._h, int(gp_id), z.data_ptr(), P, mean.data_ptr(),
+                                               grad.data_ptr(), self._stream()))
+        return mean, grad
+
     def set_tightening(self, enabled: bool, prob: float = 0.95, Ad=None, Bd=None, K=None):
         if not enabled:
             _lib.check(self.lib.gpmpc_set_tightening(self._h, 0, 0.0, None, None, None))

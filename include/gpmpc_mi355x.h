@@ -122,6 +122,13 @@ gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, d
 gpmpc_status gpmpc_gp_predict(gpmpc_handle* h, int32_t gp_id, const double* Z, int32_t P, double* mean,
                               double* var, int32_t with_noise, void* stream);
 
+/* GP mean and its input gradient at P points Z [P][d] (device): mean [P], grad [P][d] (either
+ * may be NULL), through the MFMA tile sums the SQP linearisation uses (sqp_kernel.hip
+ * gp_tiles).  Replaces the casadi mean export gpytorch_predict2casadi (gpmpc/gp.py:72-85) and
+ * the CasADi AD of it inside setup_acados_model (gpmpc/gpmpc.py:189-209). */
+gpmpc_status gpmpc_gp_mean_grad(gpmpc_handle* h, int32_t gp_id, const double* Z, int32_t P, double* mean,
+                                double* grad, void* stream);
+
 /* Handle-free GP posterior (GaussianProcess.predict() of the build): GP data already on the
  * device in the kernel layout -- rows [npad][4] = (x0, x1, x2 zero padded, alpha) and
  * linvT [npad][npad] = (L^-1)^T zero padded (NULL -> mean only), npad = n rounded up to 16.

@@ -45,6 +45,37 @@ def test_gp_predict_matches_oracle(name, N):
         assert np.abs(v - vo).max() <= 1e-9 * gpo[g].sf2, (g, np.abs(v - vo).max())
 
 
+@pytest.mark.parametrize("name,N,M", [("quad2d", 200, None), ("quad2d", 17, None), ("cartpole", 50, None),
+                                      ("quad3d", 120, 60)])
+def test_linearisation_gp_mean_grad_matches_oracle(name, N, M):
+    """The SQP linearisation's GP sums (MFMA tile path, centred inputs) vs the oracle's
+    mean_grad: |dm| <= 1e-10 sf2 sum|alpha|, |dgrad| <= 1e-9 sf2 sum|alpha| / ell^2."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(name, N)
+    gpo = oracle_gps(data, hyp)
+    gpp = product_gps(data, hyp)
+    fitc = fitc_weights(gpp, M) if M else None
+    if fitc is not None:
+        gpo = fitc_oracle_gps(gpo, fitc)
+    solver = BatchSolver(spec, 10, 1)
+    solver.set_gps(gpp, fitc=fitc)
+    rng = np.random.default_rng(11)
+    for g in range(spec.n_gp):
+        X = data[g][0]
+        Z = X[rng.integers(0, N, 150)] + 0.3 * rng.standard_normal((150, X.shape[1]))
+        Z = np.vstack([Z, X[:3], 50.0 + X[:2]])  # on the data and far away (mean 0)
+        m, gr = solver.gp_mean_grad(g, torch.tensor(Z, device="cuda"))
+        m, gr = m.cpu().numpy(), gr.cpu().numpy()
+        ref = [gpo[g].mean_grad(z) for z in Z]
+        mo = np.array([r[0] for r in ref])
+        go = np.array([r[1] for r in ref])
+        scale = gpo[g].sf2 * np.abs(gpo[g].alpha).sum()
+        assert np.abs(m - mo).max() <= 1e-10 * scale, (g, np.abs(m - mo).max(), scale)
+        assert np.abs(gr - go).max() <= 1e-9 * scale / gpo[g].ell**2, (g, np.abs(gr - go).max())
+
+
 def test_gp_predict_edge_cases():
     torch = _torch()
     spec, data, hyp = problem("quad2d", 17)  # n not a multiple of 16: padded rows
