@@ -245,7 +245,9 @@ def main():
                                  "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
                                  "Riccati recursion"},
             "roofline_variance": None if var_tf is None else {
-                "kernel": "gp_post_kernel<true>", "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
+                "kernel": (f"gp_var_tri_kernel<{(N + 15) // 16},true>" if (N + 15) // 16 <= 16
+                           else "gp_post_kernel<true>"),
+                "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},
             "kernel_ms_per_step": {"sqp": sqp_ms, "variance": var_ms},
             "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,

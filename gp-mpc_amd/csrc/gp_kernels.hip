@@ -188,6 +188,122 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
     }
 }
 
+// ---------------------------------------------------------------------------- variance, N <= 256
+// The variance-only launch for small training sets (npad <= 256, i.e. NT <= 16 column tiles:
+// config 2/3 and the per-step tightening) with every loop bound known at compile time: the
+// panel loop is unrolled, so the triangle skip costs no branches and the compiler can hoist
+// the B-fragment LDS reads and the next panel's training rows over the MFMAs.  Same math and
+// layout as gp_post_kernel: 8 wavefronts x 16 points, (L^-1)^T panels double-buffered in LDS.
+template <int NT, bool FROM_STATE>
+__global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch pb) {
+    extern __shared__ __attribute__((aligned(16))) double panel[];
+    constexpr int W = 16 * (NT | 1);   // odd number of 16-column tiles: conflict-free B fragments
+    const GPDev& g = pb.g[blockIdx.y];
+    const PostArgs& a = pb.a[blockIdx.y];
+    if ((int)blockIdx.x * kPostWaves * 16 >= a.P) return;   // uniform
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lc = lane & 15, kq = lane >> 4;
+    const int p0 = (blockIdx.x * kPostWaves + wave) * 16;
+    const int p = p0 + lc;
+    double z[3];
+    load_point<FROM_STATE>(a, p < a.P ? p : a.P - 1, z);
+    const double c = -0.5 * g.inv_ell2, sf2 = g.sf2;
+    const int npad = 16 * NT;
+    const double4* rows = reinterpret_cast<const double4*>(g.vrows);
+    // staged copy of panel q (rows 16q.., columns >= 16q)
+    double2 stage[4];
+    auto fetch = [&](int q) {
+        const int w = 16 * (NT - q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 2 * (tid + j * 64 * kPostWaves);
+            const int row = e / w, col = e - row * w;
+            stage[j] = (row < 16) ? *reinterpret_cast<const double2*>(g.linvT + (size_t)(16 * q + row) * npad + 16 * q + col)
+                                  : double2{0.0, 0.0};
+        }
+    };
+    auto deposit = [&](int q, double* buf) {
+        const int w = 16 * (NT - q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 2 * (tid + j * 64 * kPostWaves);
+            const int row = e / w, col = e - row * w;
+            if (row < 16) *reinterpret_cast<double2*>(buf + row * W + 16 * q + col) = stage[j];
+        }
+    };
+    double4 rw[4];
+    auto load_rows = [&](int q) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) rw[ks] = rows[16 * q + 4 * ks + kq];
+    };
+    f64x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    fetch(0);
+    load_rows(0);
+    deposit(0, panel);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        const double* buf = panel + (q & 1) * 16 * W;
+        double kv[4];   // k(z_point, x_row) for the four K-steps of the panel (independent exps)
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const double d0 = rw[ks].x - z[0], d1 = rw[ks].y - z[1], d2 = rw[ks].z - z[2];
+            kv[ks] = sf2 * exp_rbf(c * fma(d0, d0, fma(d1, d1, d2 * d2)));
+        }
+        if (q + 1 < NT) {
+            fetch(q + 1);
+            load_rows(q + 1);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const double* brow = buf + (4 * ks + kq) * W + lc;
+#pragma unroll
+            for (int t = q; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv[ks], brow[16 * t], acc[t], 0, 0, 0);
+        }
+        if (q + 1 < NT) deposit(q + 1, panel + ((q + 1) & 1) * 16 * W);
+        __syncthreads();
+    }
+    // acc[t][r] = V[point kq + 4r][column 16 t + lc]
+    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sq[r] = fma(acc[t][r], acc[t][r], sq[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sq[r] = dpp_row_sum(sq[r]);
+    if (lc == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int pr = p0 + kq + 4 * r;
+            if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = sf2 - sq[r] + (a.with_noise ? g.sn2 : 0.0);
+        }
+    }
+}
+
+template <bool FROM_STATE, int NT = 1>
+hipError_t launch_var_tri(const PostBatch& pb, int ntile, int blocks, hipStream_t stream) {
+    if constexpr (NT <= kMaxCT) {
+        if (ntile == NT) {
+            static bool attr = false;
+            const int lds = 2 * 16 * 16 * (NT | 1) * (int)sizeof(double);
+            if (!attr) {
+                const hipError_t e = hipFuncSetAttribute((const void*)gp_var_tri_kernel<NT, FROM_STATE>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                if (e != hipSuccess) return e;
+                attr = true;
+            }
+            hipLaunchKernelGGL((gp_var_tri_kernel<NT, FROM_STATE>), dim3(blocks, pb.n), dim3(64 * kPostWaves), lds,
+                               stream, pb);
+            return hipGetLastError();
+        }
+        return launch_var_tri<FROM_STATE, NT + 1>(pb, ntile, blocks, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream) {
     int blocks = 0;
     size_t lds = 0;
@@ -197,6 +313,14 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
             lds = std::max(lds, (size_t)2 * 16 * post_stride(post_ct(pb.npad[q])) * sizeof(double));
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
+    bool tri = true;   // every entry variance-only with the same npad <= 256
+    for (int q = 0; q < pb.n; ++q)
+        tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&
+              pb.npad[q] == pb.npad[0] && pb.npad[q] <= 16 * kMaxCT;
+    if (tri) {
+        return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, stream)
+                          : launch_var_tri<false>(pb, pb.npad[0] / 16, blocks, stream);
+    }
     static bool attr = false;
     if (!attr) {
         const int mx = 2 * 16 * post_stride(kMaxCT) * (int)sizeof(double);
