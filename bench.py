@@ -53,42 +53,54 @@ def gp_flops(spec, n_train, H):
     return per_lin, exps_lin, var
 
 
+def cpu_threads() -> int:
+    """Host cores this process may use (the GPU box exports OMP_NUM_THREADS = its CPU share)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats):
-    """Time the CPU oracle (numpy, 1 core) on a bounded closed-loop sample."""
+    """Time the C++ CPU restatement (oracle/cpu_ref.cpp: SQP-GN + Mehrotra IPM with Riccati
+    Newton steps, OpenMP over instances) on a bounded closed-loop sample of the same workload:
+    all host cores over a batch of 4 instances per thread (value), and one instance on one core
+    (the reference's usage pattern).  The first, cold step of each run is not timed
+    (gpmpc/plotting.py:25)."""
+    from oracle import cpu_ref
     from oracle import gpmpc_oracle as O
     from gpmpc.synthetic import initial_states
 
-    sd = spec.to_dict()
     gps = [O.ExactGP(X, y, *hyp[i]) for i, (X, y) in enumerate(data)]
-    sol = O.SQPSolver(sd, O.Dynamics(sd, gps), H)
-    plant = O.Dynamics(sd, None, params=spec.true_params)
+    plant = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
     traj = spec.reference_trajectory()
-    x0, phase = initial_states(spec, traj, 1)
-    x = x0[0]
-    prev = None
-    times = []
-    t_start = time.perf_counter()
-    step = 0
-    while time.perf_counter() - t_start < seconds or step < 3:
-        t0 = time.perf_counter()
-        if prev is not None:
-            sc, ic = O.propagate_constraint_limits(sd, gps, prev[0], prev[1], *lqr_mats, 0.95)
-        else:
-            sc, ic = np.zeros((2 * spec.nx, H + 1)), np.zeros((2 * spec.nu, H))
-        lbx, ubx, lbu, ubu = O.stage_bounds(sd, sc, ic, -1e-8)
-        win = O.reference_window(traj, int(phase[0]) + step, H)
-        yref = np.zeros((H + 1, spec.nx + spec.nu))
-        yref[:, :spec.nx] = win.T
-        yref[:H, spec.nx:] = spec.u_eq
-        sol.solve(x, yref, lbx, ubx, lbu, ubu)
-        times.append(time.perf_counter() - t0)
-        prev = (sol.x.T.copy(), sol.u.T.copy())
-        x = plant.rk4(x, sol.u[0])[0]
-        step += 1
-    t = np.array(times[1:])  # drop the first step (gpmpc/plotting.py:25)
-    return {"value": float(1.0 / t.mean()), "unit": "control steps/s", "cores": 1, "kind": "port",
-            "sample": f"numpy oracle (dense-KKT IPM), 1 instance, {len(t)} closed-loop steps after the first, "
-                      f"{spec.name} N={data[0][0].shape[0]} H={H}"}
+
+    def run(B, threads, budget):
+        ref = cpu_ref.CpuRef(spec, H, B, gps=gps, lqr_mats=lqr_mats)
+        x0, phase = initial_states(spec, traj, B)
+        steps, elapsed, k = 0, 0.0, 0
+        while elapsed < budget or steps < 2:
+            t0 = time.perf_counter()
+            u0 = ref.step(x0, phase + k, threads=threads)
+            dt = time.perf_counter() - t0
+            if k > 0:
+                steps += 1
+                elapsed += dt
+            for b in range(B):
+                x0[b] = plant.rk4(x0[b], u0[b])[0]
+            k += 1
+        return B * steps / elapsed, steps, ref
+
+    threads = cpu_threads()
+    Bc = 4 * threads
+    v_all, n_all, ref = run(Bc, threads, 0.65 * seconds)
+    v_one, n_one, _ = run(1, 1, 0.35 * seconds)
+    return {"value": float(v_all), "unit": "control steps/s", "cores": threads, "kind": "port",
+            "single_instance_1core": float(v_one),
+            "sample": f"C++ restatement (oracle/cpu_ref.cpp, -O3 AVX2, OpenMP), {spec.name} N={data[0][0].shape[0]} "
+                      f"H={H} exact GP: {Bc} instances x {n_all} closed-loop steps on {threads} threads; "
+                      f"single_instance_1core: 1 instance x {n_one} steps on 1 thread; first step of each run "
+                      f"untimed; sqp_iter mean {float(ref.sqp_iter.mean()):.2f}"}
 
 
 def main():
@@ -220,7 +232,7 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
         cpu = None
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and not args.fitc:
             cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats)
         out = {
             "metric": METRIC,
