@@ -390,7 +390,7 @@ struct SqpKernel {
     // then build tangent column blocks jb with jb % C == c.  Lane s (chunk 0) returns F_s and
     // G'_s[:, 0:NB] = [A_s B_s] lands in LDS.
     __device__ static void linearize(const ProblemDev& P, const Lds& L, int H, int lane, const double (&w)[NB],
-                                     double (&F)[NX]) {
+                                     double (&F)[NX], unsigned long long* tgp) {
         const int C = max(1, 64 / H);
         const int stage = lane % H;
         const int chunk = lane < C * H ? lane / H : C;  // chunk C: empty training range
@@ -403,7 +403,13 @@ struct SqpKernel {
         const double h = P.dt;
         double xs[4][NX], gm[4][NGP], gg[4][NGP][3];
         double gm0[NGP], gg0[NGP][3];
+#ifdef GPMPC_TIMING
+        unsigned long long tg0 = __builtin_amdgcn_s_memtime();
+#endif
         eval_gps(P, L, false, x, u, stage, lane, H, gm0, gg0);  // GPs of u only: once per stage
+#ifdef GPMPC_TIMING
+        *tgp += __builtin_amdgcn_s_memtime() - tg0;
+#endif
         double kprev[NX], acc[NX];
         const double cs[4] = {0.0, 0.5, 0.5, 1.0}, ws[4] = {1.0, 2.0, 2.0, 1.0};
 #pragma unroll
@@ -415,7 +421,13 @@ struct SqpKernel {
                 gm[s][g] = gm0[g];
                 gg[s][g][0] = gg0[g][0]; gg[s][g][1] = gg0[g][1]; gg[s][g][2] = gg0[g][2];
             }
+#ifdef GPMPC_TIMING
+            tg0 = __builtin_amdgcn_s_memtime();
+#endif
             eval_gps(P, L, true, xs[s], u, stage, lane, H, gm[s], gg[s]);
+#ifdef GPMPC_TIMING
+            *tgp += __builtin_amdgcn_s_memtime() - tg0;
+#endif
             M::f(P.params, xs[s], u, gm[s], kprev);
 #pragma unroll
             for (int i = 0; i < NX; ++i) acc[i] = (s == 0) ? kprev[i] : fma(ws[s], kprev[i], acc[i]);
@@ -1287,7 +1299,11 @@ struct SqpKernel {
         for (it = 0;; ++it) {
             double F[NX];
             TPHASE(1);
-            linearize(P, L, H, lane, w, F);
+#ifdef GPMPC_TIMING
+            linearize(P, L, H, lane, w, F, &tacc[11]);
+#else
+            linearize(P, L, H, lane, w, F, nullptr);
+#endif
             WSYNC();
             TPHASE(2);
             // stage reference (gpmpc.py:356-361)
