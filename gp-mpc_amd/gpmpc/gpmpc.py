@@ -56,6 +56,8 @@ class GPMPC:
         self.traj_step = 0
         self.np_random = np.random.default_rng(seed)
         self.gp_idx = self._gp_columns(spec)
+        # thrust map of the quadrotors (`gpmpc/gpmpc.py:45`); cartpole has none
+        self.acc_symbolic_fn = self.setup_symbolic_acceleration(spec.prior) if "a" in spec.prior else None
         self.gaussian_process: list[GaussianProcess] | None = None
         self._requires_recompile = False
         self.prob = prob
@@ -85,11 +87,56 @@ class GPMPC:
             c += d
         return cols
 
+    # ------------------------------------------------------------------ training data
+    def setup_symbolic_acceleration(self, params: dict):
+        """Prior thrust map T_c -> a T_c + b (`gpmpc/gpmpc.py:322-325`), a numpy callable."""
+        a, b = float(params["a"]), float(params["b"])
+        return lambda thrust_cmd: a * np.asarray(thrust_cmd, dtype=np.float64) + b
+
+    def prior_dynamics(self, x: np.ndarray, u: np.ndarray) -> np.ndarray:
+        """Continuous prior f(x, u) for rows of x (n, nx), u (n, nu) (crazyflow ``fc_func``)."""
+        return self.model.prior_f(x, u)
+
+    def preprocess_data(self, x: np.ndarray, u: np.ndarray, x_next: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """GP training inputs (N, sum d_g) and targets (N, n_gp) from transitions
+        (`gpmpc/gpmpc.py:113-151`): numerically differentiated next state minus the prior.
+
+        quad3d follows the reference literally, including its constants (g = 9.81 and
+        dt = 1/60, not the model's dt) and the thrust target as the norm of the acceleration
+        minus the prior thrust map.  quad2d / cartpole apply the same recipe to their GP
+        outputs (thrust-acceleration norm and pitch rate; cart and pole accelerations).
+        """
+        x, u, x_next = (np.atleast_2d(np.asarray(a, dtype=np.float64)) for a in (x, u, x_next))
+        spec = self.model
+        if spec.name == "quad3d":
+            g, dt = 9.81, 1 / 60
+            x_dot = (x_next - x) / dt
+            acc = np.sqrt(x_dot[:, 1] ** 2 + x_dot[:, 3] ** 2 + (x_dot[:, 5] + g) ** 2)
+            acc_target = acc - self.acc_symbolic_fn(u[:, 0])
+            f = self.prior_dynamics(x, u)
+            phi_target = x_dot[:, 6] - f[:, 6]
+            theta_target = x_dot[:, 7] - f[:, 7]
+            inputs = np.column_stack([u[:, 0], x[:, 6], x[:, 9], u[:, 1], x[:, 7], x[:, 10], u[:, 2]])
+            return inputs, np.column_stack([acc_target, phi_target, theta_target])
+        dt = spec.dt
+        x_dot = (x_next - x) / dt
+        f = self.prior_dynamics(x, u)
+        z = np.hstack([x, u])
+        inputs = np.hstack([z[:, list(idx)] for idx in spec.gp_inputs])
+        if spec.name == "quad2d":
+            acc = np.sqrt(x_dot[:, 1] ** 2 + (x_dot[:, 3] + spec.gravity) ** 2)
+            targets = np.column_stack([acc - self.acc_symbolic_fn(u[:, 0]), x_dot[:, 5] - f[:, 5]])
+        else:  # cartpole: residual cart / pole accelerations
+            targets = np.column_stack([x_dot[:, 1] - f[:, 1], x_dot[:, 3] - f[:, 3]])
+        return inputs, targets
+
     # ------------------------------------------------------------------ GP management
     def train_gp(self, x: np.ndarray, y: np.ndarray, lr: float, iterations: int):
-        """Fit one GP per output column on its input columns (`gpmpc/gpmpc.py:153-164`)."""
-        x_train = torch.tensor(np.asarray(x, dtype=np.float64))
-        y_train = torch.tensor(np.asarray(y, dtype=np.float64))
+        """Fit one GP per output column on its input columns (`gpmpc/gpmpc.py:153-164`), on the
+        controller's device (the MI355X); one all-reduce of the MLL gradient per Adam step
+        when running data-parallel (gpmpc/distributed.py)."""
+        x_train = torch.tensor(np.asarray(x, dtype=np.float64), device=self.device)
+        y_train = torch.tensor(np.asarray(y, dtype=np.float64), device=self.device)
         gps = []
         from . import distributed as D
 
@@ -99,7 +146,7 @@ class GPMPC:
             if size > 1:   # data-parallel fit: one all-reduce of the MLL gradient per Adam step
                 D.fit_gp_allreduce(gp, n_train=iterations, lr=lr)
             else:
-                fit_gp(gp, n_train=iterations, lr=lr, device="cpu")
+                fit_gp(gp, n_train=iterations, lr=lr, device=self.device)
             gps.append(gp)
         self.set_gaussian_processes(gps)
 
@@ -111,25 +158,26 @@ class GPMPC:
         self._requires_recompile = True
 
     def precompute_sparse_posterior_mean(self, n_samples: int):
-        """FITC weights on random training rows (`gpmpc/gpmpc.py:377-400`)."""
+        """FITC weights on random training rows (`gpmpc/gpmpc.py:377-400`), computed where the
+        GP lives (the MI355X for a GP fitted by ``train_gp``)."""
         gps = self.gaussian_process
         n = gps[0].train_inputs[0].shape[0]
         rand_idx = self.np_random.choice(range(n), size=n_samples, replace=False)
         out = []
         for gp in gps:
-            X = gp.train_inputs[0].cpu()
-            y = gp.train_targets.cpu()
-            S = X[rand_idx]
+            X = gp.train_inputs[0]
+            y = gp.train_targets
+            S = X[torch.as_tensor(rand_idx, device=X.device)]
             with torch.no_grad():
-                K = gp.K.cpu()
+                K = gp.K.to(X.device)
                 K_ss = gp.kernel(S)
                 K_xs = gp.kernel(X, S)
-                Gamma = torch.diagonal(K - K_xs @ torch.linalg.solve(K_ss, K_xs.T))
-                Gamma_inv = torch.diag_embed(1 / Gamma)
-                Sigma_inv = K_ss + K_xs.T @ Gamma_inv @ K_xs
-                w = torch.linalg.solve(Sigma_inv, K_xs.T) @ Gamma_inv @ y
+                Gamma = torch.diagonal(K) - (K_xs * torch.linalg.solve(K_ss, K_xs.T).T).sum(1)
+                KG = K_xs.T / Gamma            # K_sx Lambda^-1 without the dense diagonal matrix
+                Sigma_inv = K_ss + KG @ K_xs
+                w = torch.linalg.solve(Sigma_inv, KG @ y)
             # the solver evaluates sf2 * sum_j w_j exp(.): the reference's covSE already carries sf2
-            out.append((S.numpy(), w.numpy()))
+            out.append((S.cpu().numpy(), w.cpu().numpy()))
         return out
 
     # ------------------------------------------------------------------ control

@@ -160,6 +160,41 @@ class ModelSpec:
             A[3, 2], A[3, 3], B[3, 0] = dtha
         return A, B
 
+    def prior_f(self, x: np.ndarray, u: np.ndarray, params: dict | None = None) -> np.ndarray:
+        """Continuous-time prior dynamics f(x, u) for row-stacked states (n, nx) and inputs (n, nu)
+        -- crazyflow's ``fc_func`` as used by `gpmpc/gpmpc.py:87,139,145,199` (``prior_dynamics``)."""
+        p = self.prior if params is None else params
+        x = np.atleast_2d(np.asarray(x, dtype=np.float64))
+        u = np.atleast_2d(np.asarray(u, dtype=np.float64))
+        f = np.zeros_like(x)
+        g = self.gravity
+        if self.model_id == MODEL_QUAD2D:
+            th = x[:, 4]
+            acc = p["a"] * u[:, 0] + p["b"]
+            f[:, 0], f[:, 1], f[:, 2], f[:, 3] = x[:, 1], acc * np.sin(th), x[:, 3], acc * np.cos(th) - g
+            f[:, 4], f[:, 5] = x[:, 5], p["f"] * th + p["h"] * x[:, 5] + p["l"] * u[:, 1]
+        elif self.model_id == MODEL_QUAD3D:
+            phi, th, psi = x[:, 6], x[:, 7], x[:, 8]
+            acc = p["a"] * u[:, 0] + p["b"]
+            cf, sf, ct, st, cp, sp = np.cos(phi), np.sin(phi), np.cos(th), np.sin(th), np.cos(psi), np.sin(psi)
+            f[:, 0], f[:, 2], f[:, 4] = x[:, 1], x[:, 3], x[:, 5]
+            f[:, 1] = acc * (cf * st * cp + sf * sp)
+            f[:, 3] = acc * (cf * st * sp - sf * cp)
+            f[:, 5] = acc * cf * ct - g
+            f[:, 6], f[:, 7], f[:, 8] = x[:, 9], x[:, 10], x[:, 11]
+            f[:, 9] = p["c"] * phi + p["d"] * x[:, 9] + p["e"] * u[:, 1]
+            f[:, 10] = p["f"] * th + p["h"] * x[:, 10] + p["l"] * u[:, 2]
+            f[:, 11] = p["c"] * psi + p["d"] * x[:, 11] + p["e"] * u[:, 3]
+        elif self.model_id == MODEL_CARTPOLE:
+            mc, mp, l = p["m_c"], p["m_p"], p["l"]
+            M = mc + mp
+            th, w, F = x[:, 2], x[:, 3], u[:, 0]
+            s, c = np.sin(th), np.cos(th)
+            tmp = (F + mp * l * w * w * s) / M
+            tha = (g * s - c * tmp) / (l * (4.0 / 3.0 - mp * c * c / M))
+            f[:, 0], f[:, 1], f[:, 2], f[:, 3] = x[:, 1], tmp - mp * l * tha * c / M, w, tha
+        return f
+
     # ------------------------------------------------------------------ references
     def reference_trajectory(self, length: int | None = None) -> np.ndarray:
         """Periodic reference trajectory (nx, L).  The reference takes it from the

@@ -256,6 +256,32 @@ def main():
     out["cstr_sym"] = sym
     out["cstr_rows"] = np.asarray(rgpmpc.GPMPC.setup_constraints(sym, spec.x_lo, spec.x_hi)).ravel()
 
+    # ---- f(3): GPMPC.preprocess_data (training targets), prior supplied by the build's spec --
+    n = 25
+    px = np.zeros((n, 12))
+    px[:, [0, 2, 4]] = rng.uniform(-1, 1, (n, 3))
+    px[:, [1, 3, 5]] = 0.5 * rng.standard_normal((n, 3))
+    px[:, 6:9] = 0.2 * rng.standard_normal((n, 3))
+    px[:, 9:12] = 0.5 * rng.standard_normal((n, 3))
+    pu = np.column_stack([rng.uniform(0.15, 0.55, n), rng.uniform(-0.4, 0.4, (n, 3))])
+    pxn = px + 0.02 * rng.standard_normal((n, 12))
+
+    class _Arr:
+        def __init__(self, a):
+            self.a = np.asarray(a)
+
+        def full(self):
+            return self.a
+
+        def toarray(self):
+            return self.a
+
+    me4 = types.SimpleNamespace(
+        acc_symbolic_fn=lambda T: _Arr(spec.prior["a"] * np.asarray(T) + spec.prior["b"]),
+        prior_dynamics=lambda x, u: {"f": _Arr(spec.prior_f(x.T, u.T).T)})
+    pin, pout = rgpmpc.GPMPC.preprocess_data(me4, px, pu, pxn)
+    out["pp_x"], out["pp_u"], out["pp_xn"], out["pp_in"], out["pp_out"] = px, pu, pxn, pin, pout
+
     np.savez(HERE / "golden_quad3d.npz", **out)
     print("wrote", HERE / "golden_quad3d.npz", "keys:", len(out))
 

@@ -211,3 +211,46 @@ def test_synthetic_data_is_seeded():
         np.testing.assert_array_equal(ya, yb)
     x0, ph = initial_states(s, s.reference_trajectory(), 1030)
     assert ph[1029] == 1029 % s.traj_len and x0.shape == (1030, 6)
+
+
+def test_preprocess_data_matches_reference_fixture(golden3d):
+    """GPMPC.preprocess_data vs the reference's own preprocess_data (`gpmpc/gpmpc.py:113-151`)
+    run by tests/golden/make_golden.py with the build's quad3d prior plugged in as
+    crazyflow's fc_func (the part under test is the target construction)."""
+    from gpmpc.gpmpc import GPMPC
+    from gpmpc.models import get_spec
+
+    g = golden3d
+    me = GPMPC.__new__(GPMPC)
+    me.model = get_spec("quad3d")
+    me.acc_symbolic_fn = GPMPC.setup_symbolic_acceleration(me, me.model.prior)
+    inp, out = GPMPC.preprocess_data(me, g["pp_x"], g["pp_u"], g["pp_xn"])
+    np.testing.assert_allclose(inp, g["pp_in"], rtol=0, atol=0)
+    np.testing.assert_allclose(out, g["pp_out"], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["quad2d", "cartpole"])
+def test_preprocess_data_recovers_gp_residual(name):
+    """quad2d / cartpole analogue: transitions of the true plant (Euler, so the finite difference
+    is exact) give targets equal to true-minus-prior dynamics on the GP outputs."""
+    from gpmpc.gpmpc import GPMPC
+    from gpmpc.models import get_spec
+
+    spec = get_spec(name)
+    rng = np.random.default_rng(3)
+    n = 40
+    x = 0.1 * rng.standard_normal((n, spec.nx))
+    u = spec.u_eq + 0.05 * rng.standard_normal((n, spec.nu))
+    xn = x + spec.dt * spec.prior_f(x, u, spec.true_params)
+    me = GPMPC.__new__(GPMPC)
+    me.model = spec
+    me.acc_symbolic_fn = GPMPC.setup_symbolic_acceleration(me, spec.prior) if "a" in spec.prior else None
+    inp, tgt = GPMPC.preprocess_data(me, x, u, xn)
+    assert inp.shape == (n, sum(spec.gp_dims)) and tgt.shape == (n, spec.n_gp)
+    ft, fp = spec.prior_f(x, u, spec.true_params), spec.prior_f(x, u)
+    if name == "quad2d":
+        acc_t = np.sqrt(ft[:, 1] ** 2 + (ft[:, 3] + spec.gravity) ** 2)
+        np.testing.assert_allclose(tgt[:, 0], acc_t - (spec.prior["a"] * u[:, 0] + spec.prior["b"]), atol=1e-9)
+        np.testing.assert_allclose(tgt[:, 1], ft[:, 5] - fp[:, 5], atol=1e-9)
+    else:
+        np.testing.assert_allclose(tgt, (ft - fp)[:, [1, 3]], atol=1e-9)
