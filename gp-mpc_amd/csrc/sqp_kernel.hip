@@ -1173,8 +1173,6 @@ struct SqpKernel {
         }
     }
 
-    // largest alpha with v + alpha dv >= 0 (v > 0); reciprocal instead of an IEEE division sequence
-    __device__ static double max_step(double v, double dv) { return dv < 0.0 ? v * fast_rcp(-dv) : 1e300; }
 
     // cost Hessian diagonal of stage variable v on lane k (acados cost_scaling: dt on stages, 1 terminal)
     __device__ static double hdiag(const ProblemDev& P, int v, int lane, int H) {
@@ -1371,6 +1369,14 @@ struct SqpKernel {
             for (qit = 0; qit < P.qp_max_iter; ++qit) {
                 double rp[NX];
                 TPHASE(10);
+                // slack reciprocals, once per IPM iteration: every later 1/s of this iteration
+                // and the ratio-test step lengths (1 / max(-ds/s)) reuse them
+                double isl[NB], isu[NB];
+#pragma unroll
+                for (int v = 0; v < NB; ++v) {
+                    isl[v] = fast_rcp(sl[v]);
+                    isu[v] = fast_rcp(su[v]);
+                }
                 {
                     double ctq[NB];
                     ctpi(L, H, lane, piq, ctq);
@@ -1387,9 +1393,8 @@ struct SqpKernel {
                         mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
                         if (on) {
                             // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
-                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
-                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] * isl + lu[v] * isu : 0.0);
-                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl * isl - lu[v] - lu[v] * ru * isu : 0.0;
+                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] * isl[v] + lu[v] * isu[v] : 0.0);
+                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl * isl[v] - lu[v] - lu[v] * ru * isu[v] : 0.0;
                         }
                     }
 #pragma unroll
@@ -1426,21 +1431,20 @@ struct SqpKernel {
                         TPHASE(3);
                         recover_step(L, H, lane, dd, dp);
                     }
-                    double amax = 1.0, mua_l = 0.0;
+                    // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
+                    // alpha_max = 1 / max(1, max_i -dv_i / v_i)
+                    double rmax = 1.0, mua_l = 0.0;
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
                         const bool av = v < NX ? act_x : act_u;
                         if (av) {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
-                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] - ll[v] * dsl * fast_rcp(sl[v]);
-                            const double dlu = -lu[v] - lu[v] * dsu * fast_rcp(su[v]);
-                            amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl), max_step(su[v], dsu)),
-                                                   fmin(max_step(ll[v], dll), max_step(lu[v], dlu))));
+                            const double ql = (dd[v] + rl) * isl[v], qu = (-dd[v] + ru) * isu[v];
+                            rmax = fmax(rmax, fmax(fmax(-ql, -qu), fmax(1.0 + ql, 1.0 + qu)));
                         }
                     }
-                    const double a_aff = wave_min(amax);
+                    const double a_aff = fast_rcp(wave_max(rmax));
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
                         const bool av = v < NX ? act_x : act_u;
@@ -1448,9 +1452,9 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] - ll[v] * dsl * fast_rcp(sl[v]);
-                            const double dlu = -lu[v] - lu[v] * dsu * fast_rcp(su[v]);
-                            mua_l += (ll[v] + a_aff * dll) * (sl[v] + a_aff * dsl) + (lu[v] + a_aff * dlu) * (su[v] + a_aff * dsu);
+                            const double ql = dsl * isl[v], qu = dsu * isu[v];
+                            mua_l += ll[v] * fma(-a_aff, 1.0 + ql, 1.0) * fma(a_aff, dsl, sl[v]) +
+                                     lu[v] * fma(-a_aff, 1.0 + qu, 1.0) * fma(a_aff, dsu, su[v]);
                         }
                     }
                     const double mu_aff = wave_sum(mua_l) / nc;
@@ -1466,10 +1470,9 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
-                            const double dll = -ll[v] - ll[v] * dsl * isl;
-                            const double dlu = -lu[v] - lu[v] * dsu * isu;
-                            L.gq[k * NB + v] += (dll * dsl - smu) * isl - (dlu * dsu - smu) * isu;
+                            const double dll = -ll[v] * fma(dsl, isl[v], 1.0);
+                            const double dlu = -lu[v] * fma(dsu, isu[v], 1.0);
+                            L.gq[k * NB + v] += (dll * dsl - smu) * isl[v] - (dlu * dsu - smu) * isu[v];
                         }
                     }
                     WSYNC();
@@ -1492,7 +1495,7 @@ struct SqpKernel {
                         TPHASE(3);
                         recover_step(L, H, lane, dd, dp);
                     }
-                    amax = 1.0;
+                    rmax = 1.0;
                     double dsl[NB], dsu[NB], dll[NB], dlu[NB];
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
@@ -1502,20 +1505,20 @@ struct SqpKernel {
                             const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
                             const double ru = (ubv(v) - w[v]) - d[v] - su[v];
                             const double dsla = dda[v] + rl, dsua = -dda[v] + ru;
-                            const double isl = fast_rcp(sl[v]), isu = fast_rcp(su[v]);
-                            const double dlla = -ll[v] - ll[v] * dsla * isl;
-                            const double dlua = -lu[v] - lu[v] * dsua * isu;
+                            const double dlla = -ll[v] * fma(dsla, isl[v], 1.0);
+                            const double dlua = -lu[v] * fma(dsua, isu[v], 1.0);
                             const double rml = ll[v] * sl[v] + dlla * dsla - smu;
                             const double rmu = lu[v] * su[v] + dlua * dsua - smu;
                             dsl[v] = dd[v] + rl;
                             dsu[v] = -dd[v] + ru;
-                            dll[v] = (-rml - ll[v] * dsl[v]) * isl;
-                            dlu[v] = (-rmu - lu[v] * dsu[v]) * isu;
-                            amax = fmin(amax, fmin(fmin(max_step(sl[v], dsl[v]), max_step(su[v], dsu[v])),
-                                                   fmin(max_step(ll[v], dll[v]), max_step(lu[v], dlu[v]))));
+                            dll[v] = (-rml - ll[v] * dsl[v]) * isl[v];
+                            dlu[v] = (-rmu - lu[v] * dsu[v]) * isu[v];
+                            const double ill = fast_rcp(ll[v]), ilu = fast_rcp(lu[v]);
+                            rmax = fmax(rmax, fmax(fmax(-dsl[v] * isl[v], -dsu[v] * isu[v]),
+                                                   fmax(-dll[v] * ill, -dlu[v] * ilu)));
                         }
                     }
-                    const double alpha = fmin(1.0, 0.995 * wave_min(amax));
+                    const double alpha = fmin(1.0, 0.995 * fast_rcp(wave_max(rmax)));
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
                         const bool av = v < NX ? act_x : act_u;
