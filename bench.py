@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--qp-tol", type=float, default=1e-8, help="IPM tolerance of the QP sub-problems")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
+    ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
+                    help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
     ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
                     help="tools/pmc_summary.py output of the same command (roofline.traffic)")
@@ -141,6 +143,8 @@ def main():
     from gpmpc.synthetic import DEFAULT_HYPERS, initial_states, make_training_data
 
     spec = get_spec(args.model)
+    if args.var_inputs == "dynamics":
+        spec.var_inputs = spec.gp_inputs
     H, B, N = args.horizon, args.batch, args.n_train
     data = D.replicate_training_data(make_training_data(spec, N, seed=1), device=dev)  # GP replicated on every rank
     hyp = DEFAULT_HYPERS[spec.name]
@@ -220,7 +224,8 @@ def main():
         achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
         var_ms = float(stats[2]) / max(kt["var_launches"], 1)
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if kt["var_launches"] else None
-        workload = f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}, " \
+        workload = f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}" \
+                   f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}, " \
                    f"{B} instances per GPU, closed loop"
         traffic = None
         try:

@@ -338,6 +338,16 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
     return GPMPC_OK;
 }
 
+gpmpc_status gpmpc_set_var_inputs(gpmpc_handle* h, int32_t gp_id, const int32_t* src, int32_t d) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (gp_id < 0 || gp_id >= h->md.ngp) return fail(GPMPC_ERR_ARG, "gp_id out of range");
+    if (!src || d != h->md.gp_dim[gp_id]) return fail(GPMPC_ERR_ARG, "variance input map must have the GP's dimension");
+    for (int k = 0; k < d; ++k)
+        if (src[k] < 0 || src[k] >= h->md.nx + h->md.nu) return fail(GPMPC_ERR_ARG, "variance input index out of range");
+    for (int k = 0; k < 3; ++k) h->md.var_src[gp_id][k] = k < d ? src[k] : 0;
+    return GPMPC_OK;
+}
+
 gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     if (enabled)

@@ -32,8 +32,14 @@ class GPMPC:
     def __init__(self, symbolic_model, traj: np.ndarray | None = None, prior_params: dict | None = None,
                  horizon: int = 25, q_mpc: list | None = None, r_mpc: list | None = None, sparse_gp: bool = False,
                  prob: float = 0.955, max_gp_samples: int = 30, seed: int = 1337, device: str = "cuda",
-                 output_dir: Path | None = None, batch: int = 1, **solver_kw):
+                 output_dir: Path | None = None, batch: int = 1, variance_inputs: str = "reference", **solver_kw):
         spec = symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)
+        # "reference": the variance input map of `gpmpc/gpmpc.py:437-444` (for quad3d it indexes the
+        # full state-input vector with the GP-input-space indices); "dynamics": each GP's own inputs
+        if variance_inputs == "dynamics":
+            spec.var_inputs = spec.gp_inputs
+        elif variance_inputs != "reference":
+            raise ValueError("variance_inputs must be 'reference' or 'dynamics'")
         self.model = spec
         if q_mpc is not None:
             spec.q_diag = np.asarray(q_mpc, dtype=np.float64)

@@ -80,6 +80,7 @@ class BatchSolver:
             _c(spec.r_diag).ctypes.data, _c(spec.u_eq).ctypes.data, float(uh), int(cost_scaling)))
         self.set_options(max_iter=max_iter, tol=tol, qp_max_iter=qp_max_iter, qp_tol=qp_tol, qp_mu0=qp_mu0)
         self.set_reference(spec.reference_trajectory() if traj is None else traj)
+        self.set_var_inputs(spec.var_inputs)
         self.gps: list[GaussianProcess] | None = None
         # per-step device buffers
         kw = dict(device=self.device)
@@ -143,6 +144,13 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_gp_mean_grad(self._h, int(gp_id), z.data_ptr(), P, mean.data_ptr(),
                                                grad.data_ptr(), self._stream()))
         return mean, grad
+
+    def set_var_inputs(self, var_inputs):
+        """Per-GP input map of the tightening variance (indices into z = [x; u]); see
+        gpmpc_set_var_inputs.  ``spec.var_inputs`` (the reference's map) is the default."""
+        for g, idx in enumerate(var_inputs):
+            a = np.ascontiguousarray(idx, dtype=np.int32)
+            _lib.check(self.lib.gpmpc_set_var_inputs(self._h, g, a.ctypes.data, len(a)))
 
     def set_tightening(self, enabled: bool, prob: float = 0.95, Ad=None, Bd=None, K=None):
         if not enabled:

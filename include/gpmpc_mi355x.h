@@ -90,6 +90,13 @@ gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled);
 gpmpc_status gpmpc_set_tightening(gpmpc_handle* h, int32_t enabled, double inverse_cdf, const double* Ad,
                                   const double* Bd, const double* K);
 
+/* Input map of GP gp_id's tightening variance: indices src[0..d) into z = [x; u] (d = the
+ * GP's input dimension).  The default is the reference's map, which evaluates GP g at
+ * z[:, gp_idx[g]] with gp_idx indexing the GP-input space (gpmpc/gpmpc.py:59 vs 437-444,
+ * reproduced for quad3d); passing the GP's own dynamics inputs (gpmpc/gpmpc.py:173)
+ * evaluates the variance where the mean is evaluated. */
+gpmpc_status gpmpc_set_var_inputs(gpmpc_handle* h, int32_t gp_id, const int32_t* src, int32_t d);
+
 /* Forget the previous solution for instances [0, batch): the next solve runs without
  * tightening (GPMPC.reset, gpmpc/gpmpc.py:109-111).  reset_iterate = 1 also zeroes the
  * warm-start iterate and multipliers (acados_solver.reset(), gpmpc/mpc.py:147). */

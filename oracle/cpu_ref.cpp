@@ -21,6 +21,9 @@
 // restatements agree to rounding (tests/test_cpu_ref.py).
 #include <omp.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -553,6 +556,8 @@ struct Instance {
         record(H);
     }
 
+    bool trace = false;   // diagnostic: per-iteration NLP residuals to stderr
+
     int step(const double* x0, int tstep, bool has_prev, double* u0, int& sqp_iter, int& qp_total) {
         std::vector<double> t((size_t)(H + 1) * nb, 0.0);
         if (P.tighten && has_prev) tightening(x.data(), u.data(), t.data());
@@ -588,6 +593,7 @@ struct Instance {
             for (int k = 0; k < H; ++k)
                 for (int i = 0; i < nx; ++i) re = std::max(re, std::fabs(F[k * nx + i] - xs[(k + 1) * nx + i]));
             for (int i = 0; i < nx; ++i) ri = std::max(ri, std::fabs(x0[i] - xs[i]));
+            if (trace) std::fprintf(stderr, "  sqp %d: stat %.3e eq %.3e ineq %.3e comp %.3e (qp iters so far %d)\n", it, rs, re, ri, rc, qp_total);
             if (!(rs == rs && re == re && ri == ri && rc == rc)) { status = kNaN; break; }
             if (rs <= P.tol && re <= P.tol && ri <= P.tol && rc <= P.tol) { status = kSuccess; break; }
             if (it == P.max_iter) { status = kMaxIter; break; }
@@ -722,6 +728,8 @@ int cpuref_step(void* h, int B, const double* x0, const int* tstep, double* xs, 
             I.ll.assign(ll + (size_t)b * n, ll + (size_t)(b + 1) * n);
             I.lu.assign(lu + (size_t)b * n, lu + (size_t)(b + 1) * n);
             int si = 0, qi = 0;
+            const char* tr = std::getenv("CPUREF_TRACE");   // instance index to trace
+            I.trace = tr != nullptr && std::atoi(tr) == b;
             status[b] = I.step(x0 + (size_t)b * nx, tstep[b], has_prev[b] != 0, u0 + (size_t)b * nu, si, qi);
             sqp_iter[b] = si;
             qp_iter[b] = qi;

