@@ -128,13 +128,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    # one rank per GPU (local_rank modulo the visible GPUs only matters for a rehearsal of the
+    # multi-rank path on fewer GPUs, with GPMPC_DIST_BACKEND=gloo)
+    gpu = local_rank % max(torch.cuda.device_count(), 1)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        backend = os.environ.get("GPMPC_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend=backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     from gpmpc import distributed as D
     from gpmpc.gp import GaussianProcess
@@ -237,7 +244,7 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
         cpu = None
-        if not args.no_cpu_baseline and not args.fitc:
+        if world == 1 and not args.no_cpu_baseline and not args.fitc:   # rank 0 at N=1 only
             cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats)
         out = {
             "metric": METRIC,
