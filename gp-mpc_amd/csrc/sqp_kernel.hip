@@ -176,14 +176,17 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
     const int ox = (lc * 4 + lr) * 8, ow = (lr * 4 + min(lc, 3)) * 32;
     auto ldx = [&](int t) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, ox + t * 512, 0, 0)); };
     auto ldw = [&](int t, int h) { return __builtin_amdgcn_raw_buffer_load_b128(rw, ow + t * 512 + 16 * h, 0, 0); };
-    struct Ops { double x; decltype(ldw(0, 0)) wa, wb; };
-    auto load = [&](int t, Ops& o) { o.x = ldx(t); o.wa = ldw(t, 0); o.wb = ldw(t, 1); };
-    auto tile = [&](const Ops& o) {
-        auto d = [](unsigned lo, unsigned hi) { return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32)); };
-        const double wr[4] = {d(o.wa[0], o.wa[1]), d(o.wa[2], o.wa[3]), d(o.wb[0], o.wb[1]), d(o.wb[2], o.wb[3])};
-        f64x4 a[NE];
+    struct Wops { decltype(ldw(0, 0)) a, b; };
+    auto loadw = [&](int t, Wops& w) { w.a = ldw(t, 0); w.b = ldw(t, 1); };
+    // exponent tile of training tile t (one MFMA per evaluation tile)
+    auto dist = [&](double x, f64x4 (&a)[NE]) {
 #pragma unroll
-        for (int e = 0; e < NE; ++e) a[e] = mfma64(o.x, zo[e], f64x4{czz[e], czz[e], czz[e], czz[e]});
+        for (int e = 0; e < NE; ++e) a[e] = mfma64(x, zo[e], f64x4{czz[e], czz[e], czz[e], czz[e]});
+    };
+    // exps + contraction of one training tile
+    auto finish = [&](const f64x4 (&a)[NE], const Wops& w) {
+        auto d = [](unsigned lo, unsigned hi) { return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32)); };
+        const double wr[4] = {d(w.a[0], w.a[1]), d(w.a[2], w.a[3]), d(w.b[0], w.b[1]), d(w.b[2], w.b[3])};
         double ex[NE][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -194,16 +197,29 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
 #pragma unroll
             for (int e = 0; e < NE; ++e) acc[e] = mfma64(wr[r], ex[e][r], acc[e]);
     };
-    // ping-pong operand sets (no register copies on the back edge, so no wait there)
-    Ops A, B;
-    load(0, A);
-    load(1, B);
-    for (int t = 0; t < nt; t += 2) {
-        tile(A);
-        load(t + 2, A);
-        if (t + 1 < nt) tile(B);
-        load(t + 3, B);
+    // Software pipeline, two tiles per iteration (ping-pong names, no register copies on the
+    // back edge): tile t+1's exponent MFMAs are issued before tile t's exps and contraction, so
+    // they run under that VALU work; X operands are fetched two tiles ahead, W one tile ahead.
+    // The loop body is one basic block: tiles past nt read zeros (buffer range), whose exponent
+    // is finite and whose weights contribute nothing.
+    double x0 = ldx(0), x1 = ldx(1);
+    Wops w0, w1;
+    loadw(0, w0);
+    f64x4 a0[NE], a1[NE];
+    dist(x0, a0);
+    x0 = ldx(2);
+    int t = 0;
+    for (; t + 1 < nt; t += 2) {
+        dist(x1, a1);            // tile t+1
+        x1 = ldx(t + 3);
+        loadw(t + 1, w1);
+        finish(a0, w0);          // tile t
+        dist(x0, a0);            // tile t+2
+        x0 = ldx(t + 4);
+        loadw(t + 2, w0);
+        finish(a1, w1);          // tile t+1
     }
+    if (t < nt) finish(a0, w0);  // odd tile count: the last tile
 #pragma unroll
     for (int e = 0; e < NE; ++e) out[(16 * e + lc) * 4 + lr] = acc[e][0];   // S[lr][z] (row lr = register 0)
 }
@@ -364,8 +380,10 @@ struct SqpKernel {
             constexpr int G = decltype(gi)::value;
             if (M::gp_state_dep[G] != state_pass) return;
             const GPDev& g = P.gp[G];
-            gp_tiles_dispatch(g.tX, g.tW, g.ntile, L.gz + (size_t)G * np * 4, L.gc + G * np, L.gs + (size_t)G * np * 4,
-                              lane, ne);
+            double* zb = L.gz + (size_t)G * np * 4;
+            double* cz = L.gc + G * np;
+            double* so = L.gs + (size_t)G * np * 4;
+            gp_tiles_dispatch(g.tX, g.tW, g.ntile, zb, cz, so, lane, ne);
         });
         WSYNC();
         // 3. mean sf2 S0 and input gradient sf2/ell^2 (S_{1+d} - (z_d - xbar_d) S0) of this lane's stage
@@ -1198,21 +1216,18 @@ struct SqpKernel {
         int tcur = 7;
 #endif
         // ---------------- load instance state (acados memory: iterate + multipliers)
-        double w[NB], lamL[NB], lamU[NB], pi[NX];
+        // The multipliers stay in global memory (this lane's rows of S.lam / S.pi): they are read
+        // once per SQP iteration for the residuals and written after each QP, so they hold no
+        // registers through the QP (the register file is the binding resource of this kernel).
+        double w[NB];
         const double* xg = S.x + (size_t)b * (H + 1) * NX;
         const double* ug = S.u + (size_t)b * H * NU;
+        double* lam_g = S.lam + ((size_t)b * (H + 1) + k) * 2 * NB;
+        double* pi_g = S.pi + ((size_t)b * H + (act_u ? k : 0)) * NX;
 #pragma unroll
         for (int i = 0; i < NX; ++i) w[i] = on ? xg[k * NX + i] : 0.0;
 #pragma unroll
         for (int a = 0; a < NU; ++a) w[NX + a] = act_u ? ug[k * NU + a] : 0.0;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) pi[i] = act_u ? S.pi[((size_t)b * H + k) * NX + i] : 0.0;
-#pragma unroll
-        for (int v = 0; v < NB; ++v) {
-            const bool av = v < NX ? act_x : act_u;
-            lamL[v] = av ? S.lam[((size_t)b * (H + 1) + k) * 2 * NB + v] : 0.0;
-            lamU[v] = av ? S.lam[((size_t)b * (H + 1) + k) * 2 * NB + NB + v] : 0.0;
-        }
         double x0[NX];
 #pragma unroll
         for (int i = 0; i < NX; ++i) x0[i] = io.x0[(size_t)b * NX + i];
@@ -1295,13 +1310,23 @@ struct SqpKernel {
         int status = kMaxIter, it = 0, qp_total = 0;
         double res[4] = {0, 0, 0, 0};
         for (it = 0;; ++it) {
+            double lamL[NB], lamU[NB], pi[NX];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) {
+                const bool av = v < NX ? act_x : act_u;
+                lamL[v] = av ? lam_g[v] : 0.0;
+                lamU[v] = av ? lam_g[NB + v] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) pi[i] = act_u ? pi_g[i] : 0.0;
             double F[NX];
             TPHASE(1);
 #ifdef GPMPC_TIMING
-            linearize(P, L, H, lane, w, F, &tacc[11]);
+            unsigned long long* tgp = &tacc[11];
 #else
-            linearize(P, L, H, lane, w, F, nullptr);
+            unsigned long long* tgp = nullptr;
 #endif
+            linearize(P, L, H, lane, w, F, tgp);
             WSYNC();
             TPHASE(2);
             // stage reference (gpmpc.py:356-361)
@@ -1547,11 +1572,15 @@ struct SqpKernel {
                 if (av) w[v] += d[v];
                 fin = fin && (w[v] == w[v]);
                 const bool ab = v < NX ? act_x : act_u;
-                lamL[v] = ab ? ll[v] : 0.0;
-                lamU[v] = ab ? lu[v] : 0.0;
+                if (on) {
+                    lam_g[v] = ab ? ll[v] : 0.0;
+                    lam_g[NB + v] = ab ? lu[v] : 0.0;
+                }
             }
+            if (act_u) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pi[i] = act_u ? piq[i] : 0.0;
+                for (int i = 0; i < NX; ++i) pi_g[i] = piq[i];
+            }
             if (lane == 0) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) w[i] = x0[i];
@@ -1566,20 +1595,13 @@ struct SqpKernel {
         // ---------------- write back (acados memory + x_prev/u_prev, gpmpc.py:366-368)
         double* xo = S.x + (size_t)b * (H + 1) * NX;
         double* uo = S.u + (size_t)b * H * NU;
-        if (on) {
+        if (on) {   // (the multipliers are already in S.lam / S.pi)
 #pragma unroll
             for (int i = 0; i < NX; ++i) xo[k * NX + i] = w[i];
-#pragma unroll
-            for (int v = 0; v < NB; ++v) {
-                S.lam[((size_t)b * (H + 1) + k) * 2 * NB + v] = lamL[v];
-                S.lam[((size_t)b * (H + 1) + k) * 2 * NB + NB + v] = lamU[v];
-            }
         }
         if (act_u) {
 #pragma unroll
             for (int a = 0; a < NU; ++a) uo[k * NU + a] = w[NX + a];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) S.pi[((size_t)b * H + k) * NX + i] = pi[i];
         }
         if (lane == 0) {
 #pragma unroll
