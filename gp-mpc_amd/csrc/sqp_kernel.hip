@@ -67,6 +67,13 @@ __device__ __forceinline__ double xor32_d(double v) {   // value of lane l ^ 32
     const unsigned int rl = up ? lo[0] : lo[1], rh = up ? hi[0] : hi[1];
     return __longlong_as_double(((long long)rh << 32) | rl);
 }
+// Lanes 0..31 receive the value of lane l + 32 (lanes 32..63 are left undefined).
+__device__ __forceinline__ double from_upper_half(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
+    return __longlong_as_double(((long long)(unsigned int)hi[1] << 32) | (unsigned int)lo[1]);
+}
 // Whole-wave reductions (all 64 lanes active).  Every lane ends with the bitwise-same value:
 // each step combines a lane with a partner holding the mirrored partial (commutative ops).
 template <class Op>
@@ -851,19 +858,44 @@ struct SqpKernel {
             dst[r] = (dg || gcol) ? NB : 0;
         }
         struct Stage { double g[2], d[2]; };
-        auto load_stage = [&](int k, Stage& st) {
+        // Stages are loaded in the order H-1, H-2, ..., 0: each stream steps back by its per-lane
+        // stride (one subtract per stream and stage instead of a multiply-add on the address).
+        const double* pg[2] = {gb[0] + (H - 1) * gst[0], gb[1] + (H - 1) * gst[1]};
+        const double* pd[2] = {db[0] + (H - 1) * dst[0], db[1] + (H - 1) * dst[1]};
+        auto load_stage = [&](int /* k, consecutive from H-1 down */, Stage& st) {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                st.g[q] = gb[q][k * gst[q]];
-                st.d[q] = db[q][k * dst[q]];
+                st.g[q] = *pg[q];
+                pg[q] -= gst[q];
+                st.d[q] = *pd[q];
+                pd[q] -= dst[q];
             }
         };
-        double* Pk = nullptr;
+        // Store streams, stepping back one stage per call (stages are visited H-1 .. 0); entries
+        // that are not stored go to a dummy slot with stride 0.
+        double* sp[2];
+        int sp_st[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int row = lr + 4 * r;
+            const bool st = (row < NX) && colok && ((lc == NB) || row <= lc);
+            const int idx = (lc == NB) ? NX * (NX + 1) / 2 + row : pidx(row < lc ? row : lc, row < lc ? lc : row);
+            sp[r] = st ? L.P + (H - 1) * PP + idx : L.dummy + lane;
+            sp_st[r] = st ? PP : 0;
+        }
+        const bool kst = lr < NU && colok;
+        double* sk = kst ? L.K + (H - 1) * NU * PS + lr * PS + jj : L.dummy + lane;
+        const int sk_st = kst ? NU * PS : 0;
+        const bool rst = lane < NU * NU;
+        double* srui = rst ? L.Rui + (H - 1) * NU * NU + lane : L.dummy + lane;
+        const int srui_st = rst ? NU * NU : 0;
         auto stage = [&](int k, const Stage& sd) {
             // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
             const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, 0.0, 0.0};
-            f64x4 w = mfma64(lc < NX ? pn[0] : 0.0, sd.g[0], cw);
-            w = mfma64(lc < NX ? pn[1] : 0.0, sd.g[1], w);
+            // (A operand = P' itself: its p column, lane column NB, only feeds row NB of W', which
+            // the M' product never reads, so it needs no mask)
+            f64x4 w = mfma64(pn[0], sd.g[0], cw);
+            w = mfma64(pn[1], sd.g[1], w);
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], 0.0, 0.0});
             m = mfma64(sd.g[1], w[1], m);
             // Ru = M'_uu by readlane, closed-form inverse
@@ -889,48 +921,41 @@ struct SqpKernel {
                     Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
                 }
             }
-            {
-                double rv = 0.0;
-#pragma unroll
-                for (int a = 0; a < NU; ++a)
-#pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
-                const bool st = lane < NU * NU;
-                (st ? L.Rui : L.dummy)[st ? (size_t)k * NU * NU + lane : lane] = rv;
+            {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
+                double rv = Ri[0][0];
+                if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
+                *srui = rv;
+                srui -= srui_st;
             }
-            // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry)
+            // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry).
+            // Only lanes a < NU need it (the A operand is masked), so the upper-half move needs no select.
             double mu;
             if constexpr (SG == 0) mu = m[SE];
-            else if constexpr (SG == 2) mu = xor32_d(m[SE]);
+            else if constexpr (SG == 2) mu = from_upper_half(m[SE]);
             else mu = __shfl(m[SE], (((lr + SG) & 3) << 4) | lc);
-            // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff)
+            // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff);
+            // rows a >= NU meet a zero A operand and need no mask
             double kb;
             if constexpr (NU == 1) {
                 kb = -Ri[0][0] * mu;
             } else {
+                // lane a=0: mu = M'[NX], mo = M'[NX+1]; lane a=1: mu = M'[NX+1], mo = M'[NX]
                 const double mo = xor16_d(mu);
-                const bool odd = lr & 1;
-                const double m0 = odd ? mo : mu, m1 = odd ? mu : mo;
-                kb = -fma(odd ? Ri[1][0] : Ri[0][0], m0, (odd ? Ri[1][1] : Ri[0][1]) * m1);
+                kb = -fma((lr & 1) ? Ri[1][1] : Ri[0][0], mu, Ri[0][1] * mo);
             }
-            kb = (lr < NU) ? kb : 0.0;
             // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M')
             const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);
-            Pk = L.P + (size_t)k * PP;
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int row = lr + 4 * r;
                 const bool valid = (row < NX) && colok;
                 // branch-free store: entries that are not stored go to a dummy slot
-                const bool st = valid && ((lc == NB) || row <= lc);
-                const int idx = (lc == NB) ? NX * (NX + 1) / 2 + row : pidx(row < lc ? row : lc, row < lc ? lc : row);
-                (st ? Pk : L.dummy)[st ? idx : lane] = pk[r];
+                *sp[r] = pk[r];
+                sp[r] -= sp_st[r];
                 pn[r] = valid ? pk[r] : 0.0;
             }
-            {
-                const bool st = lr < NU && colok;
-                (st ? L.K : L.dummy)[st ? (size_t)k * NU * PS + lr * PS + jj : lane] = kb;
-            }
+            *sk = kb;
+            sk -= sk_st;
         };
         // stage k's operands are loaded one stage ahead (explicit double buffer: no register
         // copies that would force the wait right after the load)
