@@ -239,7 +239,8 @@ def main():
             with open(args.pmc_summary) as fh:
                 pmc = json.load(fh)
             if pmc.get("config", {}).get("workload") == workload:
-                e = pmc["kernels"].get("gpmpc::sqp_step_kernel<%d>" % spec.model_id, {})
+                pre = "gpmpc::sqp_step_kernel<%d" % spec.model_id   # <ID> or <ID, split-layout flag>
+                e = next((v for kname, v in pmc["kernels"].items() if kname.startswith(pre)), {})
                 traffic = e.get("hbm_bytes_est")
         except (OSError, ValueError, KeyError):
             traffic = None

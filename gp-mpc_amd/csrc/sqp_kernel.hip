@@ -1217,6 +1217,69 @@ struct SqpKernel {
     }
 
 
+    // ------------------------------------------------------------------ IPM-layout helpers
+    // (lane holds stage kq's variables vb .. vb + NV - 1; SPL: halves in lanes kq and kq + 32)
+    // C' pi restricted to this lane's variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
+    template <bool SPL, int NV>
+    __device__ static void ctpi_q(const Lds& L, int H, int kq, int vb, const double (&pi)[NX], double (&out)[NV]) {
+        const int lane = threadIdx.x;
+        double pim1[NX];   // pi of stage kq - 1: the previous lane of the same half
+#pragma unroll
+        for (int i = 0; i < NX; ++i) pim1[i] = __shfl(pi[i], lane > 0 ? lane - 1 : 0);
+        const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS + vb;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int v = vb + j;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + j], pi[l], acc);
+            double pm = (j < NX) ? pim1[j < NX ? j : 0] : 0.0;
+            if constexpr (SPL) {
+                const double ph = (NV + j < NX) ? pim1[NV + j < NX ? NV + j : 0] : 0.0;
+                pm = vb ? ph : pm;
+            }
+            out[j] = (v < NB) ? (((kq < H) ? -acc : 0.0) + ((v < NX && kq >= 1 && kq <= H) ? pm : 0.0)) : 0.0;
+        }
+    }
+
+    // dyn residual of stage kq (kq < H): y_{k+1} - A_k y_k - B_k v_k - c_k for stage vectors y = [x; u]
+    template <bool SPL, int NV>
+    __device__ static void dyn_residual_q(const Lds& L, int H, int kq, const double (&d)[NV], const double (&c)[NX],
+                                          double (&r)[NX]) {
+        const int lane = threadIdx.x;
+        double df[NB], xn[NX];   // full stage vectors of stages kq and kq + 1
+#pragma unroll
+        for (int v = 0; v < NB; ++v) df[v] = SPL ? __shfl(d[v % NV], kq + 32 * (v / NV)) : d[v % NV];
+#pragma unroll
+        for (int i = 0; i < NX; ++i)
+            xn[i] = SPL ? __shfl(d[i % NV], min(kq + 1 + 32 * (i / NV), 63)) : __shfl(d[i % NV], lane < 63 ? lane + 1 : 63);
+        const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double gr[NB];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) gr[j] = G[i * GS + j];
+            double acc = xn[i] - c[i];
+#pragma unroll
+            for (int j = 0; j < NB; ++j) acc = fma(-gr[j], df[j], acc);
+            r[i] = (kq < H) ? acc : 0.0;
+        }
+    }
+
+    // Step of stage kq from the Riccati solution, restricted to this lane's variables, and dpi_kq.
+    template <int NV>
+    __device__ static void recover_q(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
+        double ddf[NB];
+        if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
+        else recover_step(L, H, kq, ddf, dp);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const double lo = ddf[j < NB ? j : 0];
+            const double up = (NV + j < NB) ? ddf[NV + j < NB ? NV + j : 0] : 0.0;
+            dd[j] = vb ? up : lo;
+        }
+    }
+
     // cost Hessian diagonal of stage variable v on lane k (acados cost_scaling: dt on stages, 1 terminal)
     __device__ static double hdiag(const ProblemDev& P, int v, int lane, int H) {
         if (v < NX) return (lane >= 1 && lane <= H) ? ((lane < H) ? P.cost_scale : 1.0) * P.q[v] : 1.0;
@@ -1224,6 +1287,8 @@ struct SqpKernel {
     }
 
     // ------------------------------------------------------------------ the kernel body
+    // SPL: the QP's per-variable state is split over two lanes per stage (needs H + 1 <= 32)
+    template <bool SPL>
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
         const int lane = threadIdx.x;
@@ -1235,6 +1300,16 @@ struct SqpKernel {
         const bool act_x = on && lane >= 1;
         const bool act_u = lane < H;
         const int k = min(lane, H);
+        // IPM lane layout (see the QP below): stage kq, variables vb .. vb + NV - 1
+        constexpr int NV = SPL ? (NB + 1) / 2 : NB;
+        const bool hi_half = SPL && lane >= 32;
+        const int kq = SPL ? (lane & 31) : lane;
+        const int vb = hi_half ? NV : 0;
+        const bool on_q = kq <= H;
+        const bool actx_q = on_q && kq >= 1;
+        const bool actu_q = kq < H;
+        const int k_q = min(kq, H);
+        auto avq = [&](int j) { const int v = vb + j; return v < NX ? actx_q : (v < NB && actu_q); };
 #ifdef GPMPC_TIMING
         unsigned long long tacc[kPhases] = {};
         unsigned long long tlast = __builtin_amdgcn_s_memtime();
@@ -1249,6 +1324,7 @@ struct SqpKernel {
         const double* ug = S.u + (size_t)b * H * NU;
         double* lam_g = S.lam + ((size_t)b * (H + 1) + k) * 2 * NB;
         double* pi_g = S.pi + ((size_t)b * H + (act_u ? k : 0)) * NX;
+        double* lam_q = S.lam + ((size_t)b * (H + 1) + k_q) * 2 * NB;   // this lane's stage in the IPM layout
 #pragma unroll
         for (int i = 0; i < NX; ++i) w[i] = on ? xg[k * NX + i] : 0.0;
 #pragma unroll
@@ -1401,18 +1477,45 @@ struct SqpKernel {
             if (it == P.max_iter) { status = kMaxIter; break; }
 
             // ---------------- QP in the step variables (HPIPM's role), Mehrotra IPM
-            double d[NB], sl[NB], su[NB], ll[NB], lu[NB], piq[NX];
+            // IPM layout: lane l holds stage kq's variables v = vb + j (j < NV); with SPL the stage
+            // vectors are split over lanes kq and kq + 32 (NV = NB/2), halving the per-lane IPM
+            // state and the elementwise work.  qv(): variable vb + j of stage kq from a stage
+            // vector held in the lane = stage layout.
+            auto qv = [&](const double (&full)[NB], int j) {
+                const double lo = (j < NB) ? full[j < NB ? j : 0] : 0.0;
+                if constexpr (!SPL) return lo;
+                const double up = __shfl((NV + j < NB) ? full[NV + j < NB ? NV + j : 0] : 0.0, kq);
+                return hi_half ? up : lo;
+            };
+            double blo[NV], bup[NV], gv[NV], hd[NV], d[NV], sl[NV], su[NV], ll[NV], lu[NV], piq[NX], cqq[NX];
+            {
+                double lbm[NB], ubm[NB], hdf[NB], d0[NB];
 #pragma unroll
-            for (int v = 0; v < NB; ++v) {
-                const bool av = v < NX ? act_x : act_u;
-                d[v] = (lane == 0 && v < NX) ? x0[v] - w[v] : 0.0;   // dx_0 = e0 fixed
-                sl[v] = av ? fmax(w[v] - lbv(v), 1e-2) : 1.0;
-                su[v] = av ? fmax(ubv(v) - w[v], 1e-2) : 1.0;
-                ll[v] = av ? P.qp_mu0 * fast_rcp(sl[v]) : 0.0;
-                lu[v] = av ? P.qp_mu0 * fast_rcp(su[v]) : 0.0;
+                for (int v = 0; v < NB; ++v) {
+                    lbm[v] = lbv(v) - w[v];
+                    ubm[v] = ubv(v) - w[v];
+                    hdf[v] = hdiag(P, v, lane, H);
+                    d0[v] = (lane == 0 && v < NX) ? x0[v] - w[v] : 0.0;   // dx_0 = e0 fixed
+                }
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    blo[j] = qv(lbm, j);
+                    bup[j] = qv(ubm, j);
+                    gv[j] = qv(g, j);
+                    hd[j] = qv(hdf, j);
+                    d[j] = qv(d0, j);
+                    const bool av = avq(j);
+                    sl[j] = av ? fmax(-blo[j], 1e-2) : 1.0;
+                    su[j] = av ? fmax(bup[j], 1e-2) : 1.0;
+                    ll[j] = av ? P.qp_mu0 * fast_rcp(sl[j]) : 0.0;
+                    lu[j] = av ? P.qp_mu0 * fast_rcp(su[j]) : 0.0;
+                }
             }
 #pragma unroll
-            for (int i = 0; i < NX; ++i) piq[i] = 0.0;
+            for (int i = 0; i < NX; ++i) {
+                piq[i] = 0.0;
+                cqq[i] = SPL ? __shfl(cq[i], kq) : cq[i];
+            }
             bool qp_ok = true;
             int qit = 0;
             TPHASE(3);
@@ -1421,30 +1524,30 @@ struct SqpKernel {
                 TPHASE(10);
                 // slack reciprocals, once per IPM iteration: every later 1/s of this iteration
                 // and the ratio-test step lengths (1 / max(-ds/s)) reuse them
-                double isl[NB], isu[NB];
+                double isl[NV], isu[NV];
 #pragma unroll
-                for (int v = 0; v < NB; ++v) {
-                    isl[v] = fast_rcp(sl[v]);
-                    isu[v] = fast_rcp(su[v]);
+                for (int j = 0; j < NV; ++j) {
+                    isl[j] = fast_rcp(sl[j]);
+                    isu[j] = fast_rcp(su[j]);
                 }
                 {
-                    double ctq[NB];
-                    ctpi(L, H, lane, piq, ctq);
-                    dyn_residual(L, H, lane, d, cq, rp);
+                    double ctq[NV];
+                    ctpi_q<SPL, NV>(L, H, kq, vb, piq, ctq);
+                    dyn_residual_q<SPL, NV>(L, H, kq, d, cqq, rp);
                     double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        const bool av = v < NX ? act_x : act_u;
-                        const double rd = av ? fma(hdiag(P, v, lane, H), d[v], g[v]) - ll[v] + lu[v] + ctq[v] : 0.0;
-                        const double rl = av ? d[v] - (lbv(v) - w[v]) - sl[v] : 0.0;
-                        const double ru = av ? (ubv(v) - w[v]) - d[v] - su[v] : 0.0;
+                    for (int j = 0; j < NV; ++j) {
+                        const bool av = avq(j);
+                        const double rd = av ? fma(hd[j], d[j], gv[j]) - ll[j] + lu[j] + ctq[j] : 0.0;
+                        const double rl = av ? d[j] - blo[j] - sl[j] : 0.0;
+                        const double ru = av ? bup[j] - d[j] - su[j] : 0.0;
                         m_rd = fmax(m_rd, fabs(rd));
                         m_lu = fmax(m_lu, fmax(fabs(rl), fabs(ru)));
-                        mu_l += av ? ll[v] * sl[v] + lu[v] * su[v] : 0.0;
-                        if (on) {
+                        mu_l += av ? ll[j] * sl[j] + lu[j] * su[j] : 0.0;
+                        if (on_q && vb + j < NB) {
                             // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
-                            L.hq[k * NB + v] = hdiag(P, v, lane, H) + (av ? ll[v] * isl[v] + lu[v] * isu[v] : 0.0);
-                            L.gq[k * NB + v] = av ? rd + ll[v] + ll[v] * rl * isl[v] - lu[v] - lu[v] * ru * isu[v] : 0.0;
+                            L.hq[k_q * NB + vb + j] = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
+                            L.gq[k_q * NB + vb + j] = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
                         }
                     }
 #pragma unroll
@@ -1455,13 +1558,13 @@ struct SqpKernel {
                     m_lu = wave_max(m_lu);
                     if (!(mu == mu) || !(m_rd == m_rd)) { qp_ok = false; break; }
                     if (m_rd <= P.qp_tol && m_rb <= P.qp_tol && m_lu <= P.qp_tol && mu <= P.qp_tol) break;
-                    if (act_u) {
+                    if (actu_q && !hi_half) {
 #pragma unroll
-                        for (int i = 0; i < NX; ++i) L.G[(size_t)lane * NX * GS + i * GS + NB] = -rp[i];
+                        for (int i = 0; i < NX; ++i) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
                     }
                     WSYNC();
                     TPHASE(4);
-                    double dd[NB], dp[NX];
+                    double dd[NV], dp[NX];
                     if constexpr (kMfma) {
                         if (!mfma_backward(L, H, lane)) { qp_ok = false; break; }
                         WSYNC();
@@ -1472,57 +1575,54 @@ struct SqpKernel {
                         valu_forward(L, H, lane);
                         WSYNC();
                         TPHASE(9);
-                        recover_step_mfma(L, H, lane, dd, dp);
+                        recover_q<NV>(L, H, kq, vb, dd, dp);
                         TPHASE(3);
                     } else {
                         if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
                         TPHASE(6);
                         riccati_forward(L, H, lane);
                         TPHASE(3);
-                        recover_step(L, H, lane, dd, dp);
+                        recover_q<NV>(L, H, kq, vb, dd, dp);
                     }
                     // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
                     // alpha_max = 1 / max(1, max_i -dv_i / v_i)
                     double rmax = 1.0, mua_l = 0.0;
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        const bool av = v < NX ? act_x : act_u;
-                        if (av) {
-                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
-                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
-                            const double ql = (dd[v] + rl) * isl[v], qu = (-dd[v] + ru) * isu[v];
+                    for (int j = 0; j < NV; ++j) {
+                        if (avq(j)) {
+                            const double rl = d[j] - blo[j] - sl[j];
+                            const double ru = bup[j] - d[j] - su[j];
+                            const double ql = (dd[j] + rl) * isl[j], qu = (-dd[j] + ru) * isu[j];
                             rmax = fmax(rmax, fmax(fmax(-ql, -qu), fmax(1.0 + ql, 1.0 + qu)));
                         }
                     }
                     const double a_aff = fast_rcp(wave_max(rmax));
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        const bool av = v < NX ? act_x : act_u;
-                        if (av) {
-                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
-                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
-                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double ql = dsl * isl[v], qu = dsu * isu[v];
-                            mua_l += ll[v] * fma(-a_aff, 1.0 + ql, 1.0) * fma(a_aff, dsl, sl[v]) +
-                                     lu[v] * fma(-a_aff, 1.0 + qu, 1.0) * fma(a_aff, dsu, su[v]);
+                    for (int j = 0; j < NV; ++j) {
+                        if (avq(j)) {
+                            const double rl = d[j] - blo[j] - sl[j];
+                            const double ru = bup[j] - d[j] - su[j];
+                            const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
+                            const double ql = dsl * isl[j], qu = dsu * isu[j];
+                            mua_l += ll[j] * fma(-a_aff, 1.0 + ql, 1.0) * fma(a_aff, dsl, sl[j]) +
+                                     lu[j] * fma(-a_aff, 1.0 + qu, 1.0) * fma(a_aff, dsu, su[j]);
                         }
                     }
                     const double mu_aff = wave_sum(mua_l) / nc;
                     const double sr = mu_aff / mu;
                     const double smu = sr * sr * sr * mu;
                     // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu  ->  gq += (dll dsl - smu)/sl - (dlu dsu - smu)/su
-                    double dda[NB];
+                    double dda[NV];
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        dda[v] = dd[v];
-                        const bool av = v < NX ? act_x : act_u;
-                        if (on && av) {
-                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
-                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
-                            const double dsl = dd[v] + rl, dsu = -dd[v] + ru;
-                            const double dll = -ll[v] * fma(dsl, isl[v], 1.0);
-                            const double dlu = -lu[v] * fma(dsu, isu[v], 1.0);
-                            L.gq[k * NB + v] += (dll * dsl - smu) * isl[v] - (dlu * dsu - smu) * isu[v];
+                    for (int j = 0; j < NV; ++j) {
+                        dda[j] = dd[j];
+                        if (on_q && avq(j)) {
+                            const double rl = d[j] - blo[j] - sl[j];
+                            const double ru = bup[j] - d[j] - su[j];
+                            const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
+                            const double dll = -ll[j] * fma(dsl, isl[j], 1.0);
+                            const double dlu = -lu[j] * fma(dsu, isu[j], 1.0);
+                            L.gq[k_q * NB + vb + j] += (dll * dsl - smu) * isl[j] - (dlu * dsu - smu) * isu[j];
                         }
                     }
                     WSYNC();
@@ -1536,51 +1636,49 @@ struct SqpKernel {
                         valu_forward(L, H, lane);
                         WSYNC();
                         TPHASE(9);
-                        recover_step_mfma(L, H, lane, dd, dp);
+                        recover_q<NV>(L, H, kq, vb, dd, dp);
                         TPHASE(3);
                     } else {
                         riccati_vector(L, H, lane);
                         TPHASE(6);
                         riccati_forward(L, H, lane);
                         TPHASE(3);
-                        recover_step(L, H, lane, dd, dp);
+                        recover_q<NV>(L, H, kq, vb, dd, dp);
                     }
                     rmax = 1.0;
-                    double dsl[NB], dsu[NB], dll[NB], dlu[NB];
+                    double dsl[NV], dsu[NV], dll[NV], dlu[NV];
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        const bool av = v < NX ? act_x : act_u;
-                        dsl[v] = dsu[v] = dll[v] = dlu[v] = 0.0;
-                        if (av) {
-                            const double rl = d[v] - (lbv(v) - w[v]) - sl[v];
-                            const double ru = (ubv(v) - w[v]) - d[v] - su[v];
-                            const double dsla = dda[v] + rl, dsua = -dda[v] + ru;
-                            const double dlla = -ll[v] * fma(dsla, isl[v], 1.0);
-                            const double dlua = -lu[v] * fma(dsua, isu[v], 1.0);
-                            const double rml = ll[v] * sl[v] + dlla * dsla - smu;
-                            const double rmu = lu[v] * su[v] + dlua * dsua - smu;
-                            dsl[v] = dd[v] + rl;
-                            dsu[v] = -dd[v] + ru;
-                            dll[v] = (-rml - ll[v] * dsl[v]) * isl[v];
-                            dlu[v] = (-rmu - lu[v] * dsu[v]) * isu[v];
-                            const double ill = fast_rcp(ll[v]), ilu = fast_rcp(lu[v]);
-                            rmax = fmax(rmax, fmax(fmax(-dsl[v] * isl[v], -dsu[v] * isu[v]),
-                                                   fmax(-dll[v] * ill, -dlu[v] * ilu)));
+                    for (int j = 0; j < NV; ++j) {
+                        dsl[j] = dsu[j] = dll[j] = dlu[j] = 0.0;
+                        if (avq(j)) {
+                            const double rl = d[j] - blo[j] - sl[j];
+                            const double ru = bup[j] - d[j] - su[j];
+                            const double dsla = dda[j] + rl, dsua = -dda[j] + ru;
+                            const double dlla = -ll[j] * fma(dsla, isl[j], 1.0);
+                            const double dlua = -lu[j] * fma(dsua, isu[j], 1.0);
+                            const double rml = ll[j] * sl[j] + dlla * dsla - smu;
+                            const double rmu = lu[j] * su[j] + dlua * dsua - smu;
+                            dsl[j] = dd[j] + rl;
+                            dsu[j] = -dd[j] + ru;
+                            dll[j] = (-rml - ll[j] * dsl[j]) * isl[j];
+                            dlu[j] = (-rmu - lu[j] * dsu[j]) * isu[j];
+                            const double ill = fast_rcp(ll[j]), ilu = fast_rcp(lu[j]);
+                            rmax = fmax(rmax, fmax(fmax(-dsl[j] * isl[j], -dsu[j] * isu[j]),
+                                                   fmax(-dll[j] * ill, -dlu[j] * ilu)));
                         }
                     }
                     const double alpha = fmin(1.0, 0.995 * fast_rcp(wave_max(rmax)));
 #pragma unroll
-                    for (int v = 0; v < NB; ++v) {
-                        const bool av = v < NX ? act_x : act_u;
-                        if (av) {
-                            d[v] = fma(alpha, dd[v], d[v]);
-                            sl[v] = fma(alpha, dsl[v], sl[v]);
-                            su[v] = fma(alpha, dsu[v], su[v]);
-                            ll[v] = fma(alpha, dll[v], ll[v]);
-                            lu[v] = fma(alpha, dlu[v], lu[v]);
+                    for (int j = 0; j < NV; ++j) {
+                        if (avq(j)) {
+                            d[j] = fma(alpha, dd[j], d[j]);
+                            sl[j] = fma(alpha, dsl[j], sl[j]);
+                            su[j] = fma(alpha, dsu[j], su[j]);
+                            ll[j] = fma(alpha, dll[j], ll[j]);
+                            lu[j] = fma(alpha, dlu[j], lu[j]);
                         }
                     }
-                    if (act_u) {
+                    if (actu_q) {
 #pragma unroll
                         for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
                     }
@@ -1590,17 +1688,28 @@ struct SqpKernel {
             TPHASE(2);
             if (!qp_ok) { status = kQPFailure; break; }
             // full SQP step: w += d, multipliers <- QP multipliers
+            if (on_q) {
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    if (vb + j < NB) {
+                        const bool ab = avq(j);
+                        lam_q[vb + j] = ab ? ll[j] : 0.0;
+                        lam_q[NB + vb + j] = ab ? lu[j] : 0.0;
+                    }
+                }
+            }
             bool fin = true;
 #pragma unroll
             for (int v = 0; v < NB; ++v) {
-                const bool av = v < NX ? (act_x || lane == 0) : act_u;
-                if (av) w[v] += d[v];
-                fin = fin && (w[v] == w[v]);
-                const bool ab = v < NX ? act_x : act_u;
-                if (on) {
-                    lam_g[v] = ab ? ll[v] : 0.0;
-                    lam_g[NB + v] = ab ? lu[v] : 0.0;
+                // d of variable v of this lane's stage (lane = stage layout: lanes 0..31)
+                double dv = (v < NV) ? d[v < NV ? v : 0] : 0.0;
+                if constexpr (SPL) {
+                    const double up = __shfl(d[v >= NV ? v - NV : 0], lane + 32 < 64 ? lane + 32 : lane);
+                    dv = (v >= NV) ? up : dv;
                 }
+                const bool av = v < NX ? (act_x || lane == 0) : act_u;
+                if (av) w[v] += dv;
+                fin = fin && (w[v] == w[v]);
             }
             if (act_u) {
 #pragma unroll
@@ -1680,21 +1789,30 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
     return hipGetLastError();
 }
 
-template <int ID>
+template <int ID, bool SPL>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
-    SqpKernel<ID>::run(P, S, io);
+    SqpKernel<ID>::template run<SPL>(P, S, io);
+}
+
+template <int ID, bool SPL>
+hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+    const size_t lds = SqpKernel<ID>::lds_doubles(P.H) * sizeof(double);
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, SPL>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL((sqp_step_kernel<ID, SPL>), dim3(batch), dim3(64), lds, stream, P, S, io);
+    return hipGetLastError();
 }
 
 template <int ID>
 hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
-    const size_t lds = SqpKernel<ID>::lds_doubles(P.H) * sizeof(double);
-    if (lds > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(sqp_step_kernel<ID>, dim3(batch), dim3(64), lds, stream, P, S, io);
-    return hipGetLastError();
+    // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
+#ifndef GPMPC_NO_SPLIT
+    if (P.H + 1 <= 32) return launch_sqp_variant<ID, true>(P, S, io, batch, stream);
+#endif
+    return launch_sqp_variant<ID, false>(P, S, io, batch, stream);
 }
 
 size_t sqp_lds_bytes(int model, int H) {
