@@ -974,9 +974,11 @@ struct SqpKernel {
 
     // Closed-loop stage maps A'_k = [A + B K | B kff + c] (all stages in parallel); only the
     // affine column when the factorisation is unchanged (corrector).
-    __device__ static void acl_phase(const Lds& L, int H, int lane, bool full) {
-        const int cols = full ? PS : 1;
+    template <bool full>
+    __device__ static void acl_phase(const Lds& L, int H, int lane) {
+        constexpr int cols = full ? PS : 1;   // compile-time: the index splits below are multiply-shifts
         const int n = H * NX * cols;
+#pragma unroll 4
         for (int e = lane; e < n; e += 64) {
             const int k = e / (NX * cols);
             const int rem = e - k * NX * cols;
@@ -1569,7 +1571,7 @@ struct SqpKernel {
                         if (!mfma_backward(L, H, lane)) { qp_ok = false; break; }
                         WSYNC();
                         TPHASE(8);
-                        acl_phase(L, H, lane, true);
+                        acl_phase<true>(L, H, lane);
                         WSYNC();
                         TPHASE(6);
                         valu_forward(L, H, lane);
@@ -1630,7 +1632,7 @@ struct SqpKernel {
                     if constexpr (kMfma) {
                         valu_vector_backward(L, H, lane);
                         TPHASE(8);
-                        acl_phase(L, H, lane, false);
+                        acl_phase<false>(L, H, lane);
                         WSYNC();
                         TPHASE(6);
                         valu_forward(L, H, lane);

@@ -32,13 +32,13 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     WSYNC();
     KQ::mfma_backward(L, H, lane);
     WSYNC();
-    KQ::acl_phase(L, H, lane, true);
+    KQ::template acl_phase<true>(L, H, lane);
     WSYNC();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; ++r) {
         if constexpr (V == 0) KQ::mfma_backward(L, H, lane);
         if constexpr (V == 1) KQ::valu_vector_backward(L, H, lane);
-        if constexpr (V == 2) KQ::acl_phase(L, H, lane, true);
+        if constexpr (V == 2) KQ::template acl_phase<true>(L, H, lane);
         if constexpr (V == 3) KQ::mfma_forward(L, H, lane);
         if constexpr (V == 4) KQ::valu_forward(L, H, lane);
         if constexpr (V == 5) { double v = (double)r; for (int q = 0; q < H; ++q) v = wave_sum(v) * 1e-3; L.dummy[lane] = v; }
