@@ -143,17 +143,22 @@ __device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][
     return ok;
 }
 
-// GP mean + input gradient at up to 16*NE evaluation points on v_mfma_f64_16x16x4_f64
+// GP mean + input gradient at up to 16*NE evaluation points on the f64 matrix cores
 // (gpmpc/gp.py:12-14 covSE, :84-85 mean k(z,X) K^-1 y with alpha = K^-1 y precomputed).
 // Per 16-row training tile t (GPDev::tX / tW, centred on xbar) and 16-point evaluation tile:
-//   A  = X'_t Z'^T + c|z|^2           1 MFMA: X' rows [(x - xbar)/ell^2, c|x - xbar|^2], Z' columns
-//                                     [z - xbar, 1], C-init c|z - xbar|^2 (c = -1/(2 ell^2)), so A is
-//                                     the exponent c|z - x|^2 itself
+//   A  = X'_t Z'^T + c|z|^2           1 v_mfma_f64_16x16x4_f64: X' rows [(x - xbar)/ell^2, c|x - xbar|^2],
+//                                     Z' columns [z - xbar, 1], C-init c|z - xbar|^2 (c = -1/(2 ell^2)),
+//                                     so A is the exponent c|z - x|^2 itself
 //   E  = exp(A)                       4 exps per lane; register r of lane l holds
-//                                     E[x = (l>>4) + 4r][z = l&15] (C/D layout), which is the
-//                                     B operand of K-step r of the next product
-//   S += W_t^T E                      4 MFMAs (K-steps r = 0..3), W = [alpha, alpha (x - xbar)]
-// so register 0 of lane (j, z) ends with S[j][z], j < 4: {sum alpha E, sum alpha (x_d - xbar_d) E}.
+//                                     E[x = (l>>4) + 4r][z = l&15] (C/D layout)
+//   S += W_t^T E                      4 v_mfma_f64_4x4x4_4b_f64 (K-steps r = 0..3), W = [alpha,
+//                                     alpha (x - xbar)]: block b = z/4 of that instruction takes
+//                                     A[b][j][k] from lane 16k + 4b + j and B[b][k][n] from lane
+//                                     16k + 4b + n (layout probed by tools/probe_mfma4x4.hip), so
+//                                     the exps are its B operand as they lie, and D[b][j][n] lands
+//                                     in lane 16j + 4b + n: every output is a wanted S entry, a
+//                                     quarter of the 16x16x4 contraction's matrix-core cycles
+// so lane (j, z) ends with S[j][z], j < 4: {sum alpha E, sum alpha (x_d - xbar_d) E}.
 // zb: [16*NE][4] {z - xbar, 1}; czz: [16*NE] c|z - xbar|^2; out: [16*NE][4].
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int bytes) {
     const unsigned long long a = (unsigned long long)p;
@@ -172,15 +177,15 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
         zo[e] = zb[(16 * e + lc) * 4 + lr];
         czz[e] = czzb[16 * e + lc];
     }
-    f64x4 acc[NE];
+    double acc[NE];   // S[j = lr][z = 16 e + lc]
 #pragma unroll
-    for (int e = 0; e < NE; ++e) acc[e] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int e = 0; e < NE; ++e) acc[e] = 0.0;
     // Tile operands through buffer loads (SGPR resource, per-lane byte offsets): the loads are
     // intrinsics, so the two-tile prefetch below survives the IR optimiser (plain loads through
     // a phi get folded back to the use), and reads past the pack return 0.
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(tX, nt * 64 * 8);
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(tW, nt * 64 * 8);
-    const int ox = (lc * 4 + lr) * 8, ow = (lr * 4 + min(lc, 3)) * 32;
+    const int ox = (lc * 4 + lr) * 8, ow = (lr * 4 + (lc & 3)) * 32;
     auto ldx = [&](int t) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, ox + t * 512, 0, 0)); };
     auto ldw = [&](int t, int h) { return __builtin_amdgcn_raw_buffer_load_b128(rw, ow + t * 512 + 16 * h, 0, 0); };
     struct Wops { decltype(ldw(0, 0)) a, b; };
@@ -202,7 +207,7 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int e = 0; e < NE; ++e) acc[e] = mfma64(wr[r], ex[e][r], acc[e]);
+            for (int e = 0; e < NE; ++e) acc[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(wr[r], ex[e][r], acc[e], 0, 0, 0);
     };
     // Software pipeline, two tiles per iteration (ping-pong names, no register copies on the
     // back edge): tile t+1's exponent MFMAs are issued before tile t's exps and contraction, so
@@ -228,7 +233,7 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
     }
     if (t < nt) finish(a0, w0);  // odd tile count: the last tile
 #pragma unroll
-    for (int e = 0; e < NE; ++e) out[(16 * e + lc) * 4 + lr] = acc[e][0];   // S[lr][z] (row lr = register 0)
+    for (int e = 0; e < NE; ++e) out[(16 * e + lc) * 4 + lr] = acc[e];   // S[lr][z]
 }
 
 template <int N, class F, int I = 0>
