@@ -981,20 +981,40 @@ struct SqpKernel {
     // affine column when the factorisation is unchanged (corrector).
     template <bool full>
     __device__ static void acl_phase(const Lds& L, int H, int lane) {
-        constexpr int cols = full ? PS : 1;   // compile-time: the index splits below are multiply-shifts
-        const int n = H * NX * cols;
-#pragma unroll 4
-        for (int e = lane; e < n; e += 64) {
-            const int k = e / (NX * cols);
-            const int rem = e - k * NX * cols;
-            const int i = rem / cols;
-            const int j = full ? rem - i * cols : NX;
-            const double* G = L.G + (size_t)k * NX * GS + i * GS;
-            const double* Kk = L.K + (size_t)k * NU * PS;
-            double acc = (j < NX) ? G[j] : G[NB];
+        if constexpr (full) {
+            // one row (k, i) of A'_k per lane and pass: the G'_k row and K'_k are contiguous reads,
+            // the PS outputs one contiguous store
+            for (int e = lane; e < H * NX; e += 64) {
+                const int k = e / NX, i = e - k * NX;
+                const double* G = L.G + (size_t)k * NX * GS + i * GS;
+                const double* Kk = L.K + (size_t)k * NU * PS;
+                double g[GS], kr[NU][PS];
 #pragma unroll
-            for (int a = 0; a < NU; ++a) acc = fma(G[NX + a], Kk[a * PS + j], acc);
-            L.Acl[(size_t)k * NX * PS + i * PS + j] = acc;
+                for (int j = 0; j < GS; ++j) g[j] = G[j];
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j < PS; ++j) kr[a][j] = Kk[a * PS + j];
+                double* out = L.Acl + (size_t)k * NX * PS + i * PS;
+#pragma unroll
+                for (int j = 0; j < PS; ++j) {
+                    double acc = (j < NX) ? g[j] : g[NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc = fma(g[NX + a], kr[a][j], acc);
+                    out[j] = acc;
+                }
+            }
+        } else {
+#pragma unroll 4
+            for (int e = lane; e < H * NX; e += 64) {
+                const int k = e / NX, i = e - k * NX;
+                const double* G = L.G + (size_t)k * NX * GS + i * GS;
+                const double* Kk = L.K + (size_t)k * NU * PS;
+                double acc = G[NB];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) acc = fma(G[NX + a], Kk[a * PS + NX], acc);
+                L.Acl[(size_t)k * NX * PS + i * PS + NX] = acc;
+            }
         }
     }
 
