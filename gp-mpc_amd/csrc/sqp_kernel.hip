@@ -108,13 +108,14 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// 1/x to full double precision: v_rcp_f64 estimate + two Newton steps (no IEEE div sequence)
+// 1/x to full double precision (no IEEE div sequence): the v_rcp_f64 estimate r0 = (1 - eps)/x,
+// |eps| <= 2^-23, refined by one cubic step r0 (1 + e + e^2), e = 1 - x r0, whose error is eps^3.
+// Three dependent f64 ops after the estimate instead of four for two Newton steps (a dependent
+// f64 VALU op costs ~32 cycles on gfx950, tools/probe_latency.hip).
 __device__ __forceinline__ double fast_rcp(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    double e = fma(-x, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-x, r, 1.0);
-    return fma(r, e, r);
+    const double r = __builtin_amdgcn_rcp(x);
+    const double e = fma(-x, r, 1.0);
+    return fma(r, fma(e, e, e), r);
 }
 
 // In-register inverse of a small SPD matrix (Gauss-Jordan, no pivoting needed for SPD).
@@ -903,35 +904,17 @@ struct SqpKernel {
             w = mfma64(pn[1], sd.g[1], w);
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], 0.0, 0.0});
             m = mfma64(sd.g[1], w[1], m);
-            // Ru = M'_uu by readlane, closed-form inverse
-            double Ri[NU][NU];
-            {
-                double Ru[NU][NU];
+            // Ru = M'_uu by readlane.  K' = -Ru^-1 M'_u through the adjugate: the numerators are
+            // formed beside det and its reciprocal, so after det the dependency chain of the
+            // recursion is rcp -> cubic refinement -> one multiply.
+            double Ru[NU][NU];
 #pragma unroll
-                for (int a = 0; a < NU; ++a)
+            for (int a = 0; a < NU; ++a)
 #pragma unroll
-                    for (int b2 = a; b2 < NU; ++b2) {
-                        Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
-                        Ru[b2][a] = Ru[a][b2];
-                    }
-                if constexpr (NU == 1) {
-                    ok = ok && (Ru[0][0] > 0.0);
-                    Ri[0][0] = fast_rcp(Ru[0][0]);
-                } else {
-                    const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
-                    ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
-                    const double id = fast_rcp(det);
-                    Ri[0][0] = Ru[1][1] * id;
-                    Ri[1][1] = Ru[0][0] * id;
-                    Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
+                for (int b2 = a; b2 < NU; ++b2) {
+                    Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
+                    Ru[b2][a] = Ru[a][b2];
                 }
-            }
-            {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
-                double rv = Ri[0][0];
-                if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
-                *srui = rv;
-                srui -= srui_st;
-            }
             // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry).
             // Only lanes a < NU need it (the A operand is masked), so the upper-half move needs no select.
             double mu;
@@ -940,13 +923,28 @@ struct SqpKernel {
             else mu = __shfl(m[SE], (((lr + SG) & 3) << 4) | lc);
             // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff);
             // rows a >= NU meet a zero A operand and need no mask
-            double kb;
+            double kb, Ri[NU][NU];
             if constexpr (NU == 1) {
+                ok = ok && (Ru[0][0] > 0.0);
+                Ri[0][0] = fast_rcp(Ru[0][0]);
                 kb = -Ri[0][0] * mu;
             } else {
+                const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
+                ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
                 // lane a=0: mu = M'[NX], mo = M'[NX+1]; lane a=1: mu = M'[NX+1], mo = M'[NX]
                 const double mo = xor16_d(mu);
-                kb = -fma((lr & 1) ? Ri[1][1] : Ri[0][0], mu, Ri[0][1] * mo);
+                const double num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
+                const double id = fast_rcp(det);
+                kb = num * -id;
+                Ri[0][0] = Ru[1][1] * id;
+                Ri[1][1] = Ru[0][0] * id;
+                Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
+            }
+            {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
+                double rv = Ri[0][0];
+                if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
+                *srui = rv;
+                srui -= srui_st;
             }
             // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M')
             const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);

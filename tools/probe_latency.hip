@@ -43,6 +43,15 @@ __global__ void probes(double* out, long long* cyc, int iters) {
         z = __hiloint2double(hi, lo) * 0.999 + 1e-3 + l * 1e-9;
     }
     long long t9 = clock64();
+    // 5b. dependent v_mfma_f64_4x4x4_4b chain (acc -> acc) and output -> B operand
+    double q = 0.1 + l * 1e-3;
+    long long tc = clock64();
+    for (int i = 0; i < iters; ++i) q = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, q, 0, 0, 0);
+    long long td = clock64();
+    double qb = b;
+    long long te = clock64();
+    for (int i = 0; i < iters; ++i) qb = __builtin_amdgcn_mfma_f64_4x4x4f64(a, qb, 0.0, 0, 0, 0) * 1e-3 + 0.5;
+    long long tf = clock64();
     // 6. independent MFMAs (4 accumulators)
     f64x4 c0 = acc, c1 = acc, c2 = acc, c3 = acc;
     long long ta = clock64();
@@ -53,9 +62,9 @@ __global__ void probes(double* out, long long* cyc, int iters) {
         c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
     }
     long long tb = clock64();
-    out[l] = acc[0] + acc2[1] + x + y + z + c0[0] + c1[1] + c2[2] + c3[3];
+    out[l] = acc[0] + acc2[1] + x + y + z + c0[0] + c1[1] + c2[2] + c3[3] + q + qb;
     if (l == 0) {
-        cyc[0] = t1 - t0; cyc[1] = t3 - t2; cyc[2] = t5 - t4; cyc[3] = t7 - t6; cyc[4] = t9 - t8; cyc[5] = tb - ta;
+        cyc[0] = t1 - t0; cyc[1] = t3 - t2; cyc[2] = t5 - t4; cyc[3] = t7 - t6; cyc[4] = t9 - t8; cyc[5] = tb - ta; cyc[6] = td - tc; cyc[7] = tf - te;
     }
 }
 
@@ -68,9 +77,10 @@ int main() {
     probes<<<1, 64>>>(out, cyc, 10);
     probes<<<1, 64>>>(out, cyc, iters);
     long long h[8];
-    (void)hipMemcpy(h, cyc, 6 * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(h, cyc, 8 * 8, hipMemcpyDeviceToHost);
     const char* names[] = {"mfma f64 dep (acc)", "mfma f64 out->B operand", "fma f64 dep", "shfl dep",
-                           "readfirstlane dep", "mfma f64 indep x4 (per 4)"};
-    for (int i = 0; i < 6; ++i) printf("%-28s %.1f cycles/iter\n", names[i], (double)h[i] / iters);
+                           "readfirstlane dep", "mfma f64 indep x4 (per 4)", "mfma f64 4x4x4 dep (acc)",
+                           "mfma f64 4x4x4 out->B"};
+    for (int i = 0; i < 8; ++i) printf("%-28s %.1f cycles/iter\n", names[i], (double)h[i] / iters);
     return 0;
 }
