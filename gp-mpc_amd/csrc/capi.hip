@@ -64,6 +64,7 @@ struct gpmpc_handle {
     int32_t* has_prev = nullptr;
     double* traj = nullptr;
     double* plant_params = nullptr;
+    double* tgain = nullptr;        // [H][nb][n_unc] tightening gain table (ProblemDev::tgain)
     double plant_params_host[kMaxParams] = {0};
     bool plant_params_valid = false;
     double* gp_rows[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
@@ -98,7 +99,7 @@ static void free_handle(gpmpc_handle* h) {
     for (auto* v : {&h->ev_var, &h->ev_sqp})
         for (auto& pr : *v) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params})
+    for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain})
         if (p) (void)hipFree(p);
     if (h->has_prev) (void)hipFree(h->has_prev);
     if (h->scratch_i) (void)hipFree(h->scratch_i);
@@ -373,6 +374,46 @@ gpmpc_status gpmpc_set_tightening(gpmpc_handle* h, int32_t enabled, double inver
             P.Acl[i * nx + j] = acc;
         }
     for (int a = 0; a < nu * nx; ++a) P.K[a] = K[a];
+    // Gain table of the covariance convolution: column q of Acl^m Bd is column unc[q] of Acl^m
+    // (Bd selects the uncertain state dims, gpmpc.py:68-69), squared entrywise, and likewise
+    // for K Acl^m.  m = 0..H-1.
+    int32_t unc[kMaxNX];
+    const int nunc = model_unc_dims(h->model, unc);
+    const int H = h->H, nb = nx + nu;
+    std::vector<double> tab((size_t)H * nb * nunc), Am((size_t)nx * nx, 0.0), tmp((size_t)nx * nx);
+    for (int i = 0; i < nx; ++i) Am[i * nx + i] = 1.0;
+    for (int m = 0; m < H; ++m) {
+        double* t = tab.data() + (size_t)m * nb * nunc;
+        for (int q = 0; q < nunc; ++q) {
+            for (int i = 0; i < nx; ++i) {
+                const double a = Am[i * nx + unc[q]];
+                t[i * nunc + q] = a * a;
+            }
+            for (int a = 0; a < nu; ++a) {
+                double acc = 0.0;
+                for (int j = 0; j < nx; ++j) acc += K[a * nx + j] * Am[j * nx + unc[q]];
+                t[(nx + a) * nunc + q] = acc * acc;
+            }
+        }
+        for (int i = 0; i < nx; ++i)   // Am <- Acl Am
+            for (int j = 0; j < nx; ++j) {
+                double acc = 0.0;
+                for (int l = 0; l < nx; ++l) acc += P.Acl[i * nx + l] * Am[l * nx + j];
+                tmp[i * nx + j] = acc;
+            }
+        Am.swap(tmp);
+    }
+    (void)hipSetDevice(h->device);
+    if (!h->tgain) {
+        const hipError_t e = hipMalloc(&h->tgain, tab.size() * sizeof(double));
+        if (e != hipSuccess) {
+            h->tgain = nullptr;
+            P.tighten = 0;
+            return fail(GPMPC_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        }
+    }
+    HIPCHK(hipMemcpy(h->tgain, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+    P.tgain = h->tgain;
     return GPMPC_OK;
 }
 

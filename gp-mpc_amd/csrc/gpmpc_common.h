@@ -61,6 +61,10 @@ struct ProblemDev {
     double icdf;
     double Acl[kMaxNX * kMaxNX];   // A_d + B_d K_lqr (the four-term update of gpmpc.py:489-495)
     double K[kMaxNU * kMaxNX];     // K_lqr
+    // diag of Sigma_k and K Sigma_k K^T as a convolution of the per-stage GP noise (Sigma_0 = 0,
+    // Sigma_{k+1} = Acl Sigma_k Acl^T + Bd D_k Bd^T with D_k diagonal):
+    //   tgain[m][v][q] = (Acl^m Bd)_{vq}^2 (v < nx),  (K Acl^m Bd)_{v-nx,q}^2 (v >= nx),  m = 0..H-1
+    const double* tgain;
     // SQP / QP options (gpmpc.py:257-263; acados default tolerances)
     int32_t max_iter, qp_max_iter;
     double tol_stat, tol_eq, tol_ineq, tol_comp, qp_tol, qp_mu0;
@@ -142,6 +146,7 @@ struct PostBatch {
 // Launchers (sqp_kernel.hip, gp_kernels.hip).
 hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream);
 size_t sqp_lds_bytes(int model, int H);
+int model_unc_dims(int model, int32_t* unc);   // the model's uncertain state dims (Bd columns), returns their count
 hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* mean, double* grad, hipStream_t stream);
 hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream);
 hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream);

@@ -1378,49 +1378,49 @@ struct SqpKernel {
                     L.cd[lane * NUNC + j] = acc * dt2;
                 }
             }
-            double* Sig = L.Sig;
-            double* T1 = L.Sig + NX * NX;
-            double* U = L.Sig + 2 * NX * NX;
-            for (int e = lane; e < NX * NX; e += 64) Sig[e] = 0.0;
             WSYNC();
-            for (int kk = 0; kk <= H; ++kk) {
-                // record sqrt(diag Sigma_k) and sqrt(diag K Sigma_k K')
-                for (int e = lane; e < NX * NX + NU * NX; e += 64) {
-                    const bool isT = e < NX * NX;
-                    const int q = isT ? e : e - NX * NX;
-                    const int i = q / NX, j = q % NX;
-                    const double* rowA = isT ? P.Acl + i * NX : P.K + i * NX;
-                    double acc = 0.0;
+            // diag Sigma_k = sum_{m<k} sum_q tgain[m][.][q] cd_{k-1-m}[q]: the H-step covariance
+            // recursion of gpmpc.py:478-495 with Sigma_0 = 0 and diagonal noise, restated as a
+            // convolution so every stage (lane k) accumulates in parallel; tgain[m] is uniform
+            // across the wave (scalar loads), cd_{k-1-m} is the lane's LDS read.
+            double sv[NB];
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) acc = fma(rowA[m], Sig[m * NX + j], acc);
-                    (isT ? T1 : U)[q] = acc;
+            for (int v = 0; v < NB; ++v) sv[v] = 0.0;
+            constexpr int NG = NB * NUNC;
+            // k >> 8 is 0 (H < 256) but not provably uniform, so the table rows are vector loads
+            // that can be issued one term ahead (scalar loads of uniform rows were serialised by
+            // SGPR pressure); the rows come from L1.
+            const double* gbase = P.tgain + (k >> 8);
+            auto load_g = [&](int m, double (&g)[NG]) {
+#pragma unroll
+                for (int e = 0; e < NG; ++e) g[e] = gbase[(size_t)m * NG + e];
+            };
+            auto term = [&](int m, const double (&g)[NG]) {
+                const bool act = m < k && on;
+                const double* cdk = L.cd + (act ? (k - 1 - m) * NUNC : 0);   // unmasked read, masked value
+                double cdv[NUNC];
+#pragma unroll
+                for (int q = 0; q < NUNC; ++q) {
+                    const double cv = cdk[q];
+                    cdv[q] = act ? cv : 0.0;
                 }
-                if (lane < NX) L.hq[kk * NB + lane] = P.icdf * sqrt(fmax(Sig[lane * NX + lane], 0.0));
-                WSYNC();
-                if (lane < NU) {
-                    double acc = 0.0;
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) acc = fma(U[lane * NX + m], P.K[lane * NX + m], acc);
-                    L.hq[kk * NB + NX + lane] = P.icdf * sqrt(fmax(acc, 0.0));
-                }
-                if (kk == H) break;
-                for (int e = lane; e < NX * NX; e += 64) {
-                    const int i = e / NX, j = e % NX;
-                    double acc = 0.0;
+                for (int v = 0; v < NB; ++v)
 #pragma unroll
-                    for (int m = 0; m < NX; ++m) acc = fma(T1[i * NX + m], P.Acl[j * NX + m], acc);
-                    if (i == j) {
-#pragma unroll
-                        for (int q = 0; q < NUNC; ++q)
-                            if (M::unc[q] == i) acc += L.cd[kk * NUNC + q];
-                    }
-                    Sig[e] = acc;
-                }
-                WSYNC();
+                    for (int q = 0; q < NUNC; ++q) sv[v] = fma(g[v * NUNC + q], cdv[q], sv[v]);
+            };
+            double g0[NG], g1[NG];
+            load_g(0, g0);
+            int m = 0;
+            for (; m + 1 < H; m += 2) {
+                load_g(m + 1, g1);
+                term(m, g0);
+                if (m + 2 < H) load_g(m + 2, g0);
+                term(m + 1, g1);
             }
-            WSYNC();
+            if (m < H) term(m, g0);
 #pragma unroll
-            for (int v = 0; v < NB; ++v) tsd[v] = on ? L.hq[k * NB + v] : 0.0;
+            for (int v = 0; v < NB; ++v) tsd[v] = on ? P.icdf * sqrt(fmax(sv[v], 0.0)) : 0.0;
         }
         if (S.tight != nullptr && on) {
 #pragma unroll
@@ -1838,6 +1838,21 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
     if (P.H + 1 <= 32) return launch_sqp_variant<ID, true>(P, S, io, batch, stream);
 #endif
     return launch_sqp_variant<ID, false>(P, S, io, batch, stream);
+}
+
+template <int ID>
+static int unc_dims_of(int32_t* unc) {
+    for (int q = 0; q < Model<ID>::NUNC; ++q) unc[q] = Model<ID>::unc[q];
+    return Model<ID>::NUNC;
+}
+
+int model_unc_dims(int model, int32_t* unc) {
+    switch (model) {
+        case kQuad2D: return unc_dims_of<kQuad2D>(unc);
+        case kQuad3D: return unc_dims_of<kQuad3D>(unc);
+        case kCartpole: return unc_dims_of<kCartpole>(unc);
+    }
+    return 0;
 }
 
 size_t sqp_lds_bytes(int model, int H) {
