@@ -100,7 +100,32 @@ __global__ void chains(double* sink, long long* cyc, int iters, double* lds_init
         for (int u = 0; u < U; ++u) r = fma(__builtin_amdgcn_rcp(r), 0.5, 1.0);
     }
     t[n++] = clock64();
-    sink[l] = x + acc + c[0] + c[1] + a + v + r;
+    double bb = x;
+    for (int i = 0; i < iters; ++i) {   // 11 mfma out -> B operand
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            f64x4 d = __builtin_amdgcn_mfma_f64_16x16x4f64(0.5, bb, f64x4{0, 0, 0, 0}, 0, 0, 0);
+            bb = d[0];
+        }
+    }
+    t[n++] = clock64();
+    double bv = x;
+    for (int i = 0; i < iters; ++i) {   // 12 two independent mfma -> v_add -> B operand of both
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            f64x4 d0 = __builtin_amdgcn_mfma_f64_16x16x4f64(0.5, bv, f64x4{0, 0, 0, 0}, 0, 0, 0);
+            f64x4 d1 = __builtin_amdgcn_mfma_f64_16x16x4f64(0.25, bv, f64x4{0, 0, 0, 0}, 0, 0, 0);
+            bv = d0[0] + d1[1];
+        }
+    }
+    t[n++] = clock64();
+    double b4 = x;
+    for (int i = 0; i < iters; ++i) {   // 13 4x4x4_4b out -> B operand
+#pragma unroll
+        for (int u = 0; u < U; ++u) b4 = __builtin_amdgcn_mfma_f64_4x4x4f64(0.5, b4, 0.0, 0, 0, 0);
+    }
+    t[n++] = clock64();
+    sink[l] = x + acc + c[0] + c[1] + a + v + r + bb + bv + b4;
     if (l == 0)
         for (int q = 0; q + 1 < n; ++q) cyc[q] = t[q + 1] - t[q];
 }
@@ -114,12 +139,13 @@ int main() {
     const int iters = 200;
     chains<<<1, 64>>>(sink, cyc, iters, li);
     chains<<<1, 64>>>(sink, cyc, iters, li);
-    long long c[16];
+    long long c[16] = {};
     (void)hipMemcpy(c, cyc, sizeof(c), hipMemcpyDeviceToHost);
     const char* names[] = {"loop overhead / trip", "fma f64 dep", "fma f64 x4 indep (per 4)", "readlane->fma",
                            "dpp f64 -> add", "lds write->read", "shfl -> add", "mfma C chain",
-                           "mfma out -> A", "mfma out -> fma -> mfma", "rcp -> fma"};
+                           "mfma out -> A", "mfma out -> fma -> mfma", "rcp -> fma", "mfma out -> B",
+                           "2 indep mfma -> add -> B", "4x4x4_4b out -> B"};
     printf("%-28s %10.1f cycles\n", names[0], (double)c[0] / iters);
-    for (int q = 1; q < 11; ++q) printf("%-28s %10.1f cycles/link\n", names[q], (double)c[q] / iters / U);
+    for (int q = 1; q < 14; ++q) printf("%-28s %10.1f cycles/link\n", names[q], (double)c[q] / iters / U);
     return 0;
 }
