@@ -86,7 +86,8 @@ gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled);
 
 /* Constraint tightening (gpmpc/gpmpc.py:425-498): inverse_cdf (gpmpc.py:63-65) and the
  * prior LQR closed loop: Ad [nx][nx], Bd [nx][nu], K [nu][nx] (gpmpc.py:500-507).
- * enabled = 0 disables tightening (nominal MPC). */
+ * enabled = 0 disables tightening (nominal MPC).  Builds the H-term gain table of the covariance
+ * recursion on the host and copies it to the device (synchronous; a setup call). */
 gpmpc_status gpmpc_set_tightening(gpmpc_handle* h, int32_t enabled, double inverse_cdf, const double* Ad,
                                   const double* Bd, const double* K);
 
