@@ -228,7 +228,8 @@ def test_gpmpc_class_select_action_matches_oracle():
 
 
 @pytest.mark.parametrize("name,N,H,B,steps,var", [("quad3d", 100, 40, 8, 4, "dynamics"), ("quad3d", 100, 40, 8, 3, "reference"),
-                                                   ("quad2d", 200, 30, 16, 4, "reference")])
+                                                   ("quad2d", 200, 30, 16, 4, "reference"),
+                                                   ("cartpole", 50, 20, 16, 6, "reference")])
 def test_closed_loop_parity_vs_cpp_restatement(name, N, H, B, steps, var):
     """GPU vs the C++ CPU restatement (oracle/cpu_ref.cpp) in the same closed loop at KKT tol
     1e-9: identical status and SQP/QP iteration counts, |x_gpu - x_cpu| <= 1e-6 (1 + |x|).
