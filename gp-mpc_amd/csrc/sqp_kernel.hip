@@ -950,12 +950,14 @@ struct SqpKernel {
             const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
-                const int row = lr + 4 * r;
-                const bool valid = (row < NX) && colok;
                 // branch-free store: entries that are not stored go to a dummy slot
                 *sp[r] = pk[r];
                 sp[r] -= sp_st[r];
-                pn[r] = valid ? pk[r] : 0.0;
+                // P'_k is the next stage's A operand unmasked: its entries outside rows < NX and
+                // columns {< NX, NB} are finite and only reach W' rows the M' product never reads
+                // (u columns / rows >= NB) or meet the zero rows >= NX of the G' operand, so the
+                // result is the same as with them zeroed and the select stays off the chain.
+                pn[r] = pk[r];
             }
             *sk = kb;
             sk -= sk_st;
