@@ -1580,11 +1580,10 @@ struct SqpKernel {
 #pragma unroll
                     for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
                     const double mu = wave_sum(mu_l) / nc;
-                    m_rd = wave_max(m_rd);
-                    m_rb = wave_max(m_rb);
-                    m_lu = wave_max(m_lu);
-                    if (!(mu == mu) || !(m_rd == m_rd)) { qp_ok = false; break; }
-                    if (m_rd <= P.qp_tol && m_rb <= P.qp_tol && m_lu <= P.qp_tol && mu <= P.qp_tol) break;
+                    // the stopping test only needs the largest of the three residual norms: one reduction
+                    const double m_res = wave_max(fmax(m_rd, fmax(m_rb, m_lu)));
+                    if (!(mu == mu) || !(m_res == m_res)) { qp_ok = false; break; }
+                    if (m_res <= P.qp_tol && mu <= P.qp_tol) break;
                     if (actu_q && !hi_half) {
 #pragma unroll
                         for (int i = 0; i < NX; ++i) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
