@@ -819,6 +819,7 @@ struct SqpKernel {
         static_assert(NU <= 2, "MFMA Schur path handles NU <= 2");
         static_assert(NB <= 8 && NX <= 8, "stage operands occupy C elements 0..1");
         double pn[2];
+        f64x4 pq = {0.0, 0.0, 0.0, 0.0};   // P'_{k+1} as the Schur MFMA left it (rows 8..15 in [2], [3])
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
             const int row = lr + 4 * r;
@@ -897,7 +898,9 @@ struct SqpKernel {
         const int srui_st = rst ? NU * NU : 0;
         auto stage = [&](int k, const Stage& sd) {
             // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
-            const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, 0.0, 0.0};
+            // rows 8..15 of W' are never read (M' takes w[0], w[1]), so their C-init is P'_{k+1}'s own
+            // (finite) rows 8..15: the C quad is two selects on the P' quad, no zero fill
+            const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, pq[2], pq[3]};
             // (A operand = P' itself: its p column, lane column NB, only feeds row NB of W', which
             // the M' product never reads, so it needs no mask)
             f64x4 w = mfma64(pn[0], sd.g[0], cw);
@@ -959,6 +962,7 @@ struct SqpKernel {
                 // result is the same as with them zeroed and the select stays off the chain.
                 pn[r] = pk[r];
             }
+            pq = pk;
             *sk = kb;
             sk -= sk_st;
         };
