@@ -254,3 +254,35 @@ def test_preprocess_data_recovers_gp_residual(name):
         np.testing.assert_allclose(tgt[:, 1], ft[:, 5] - fp[:, 5], atol=1e-9)
     else:
         np.testing.assert_allclose(tgt, (ft - fp)[:, [1, 3]], atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["quad2d", "quad3d", "cartpole"])
+def test_tightening_convolution_matches_recursion(name):
+    """The SQP kernel's tightening (gpmpc_set_tightening's gain table + the per-stage convolution)
+    restates the reference's H-step covariance recursion (`gpmpc/gpmpc.py:478-497`,
+    Sigma_0 = 0, Sigma+ = Acl Sigma Acl' + Bd D_k Bd', D_k diagonal):
+    diag Sigma_k = sum_{m<k} (Acl^m Bd)^2 d_{k-1-m}, diag K Sigma_k K' likewise with K Acl^m Bd."""
+    s = get_spec(name)
+    Ad, Bd_, K = lqr(s)
+    Acl = Ad + Bd_ @ K
+    H, unc = 12, list(s.unc_dims)
+    Bd = np.zeros((s.nx, len(unc)))
+    Bd[unc, np.arange(len(unc))] = 1.0
+    d = np.random.default_rng(3).uniform(0.0, 1e-3, size=(H, len(unc)))
+    # reference recursion
+    Sig = np.zeros((s.nx, s.nx))
+    rec_x, rec_u = [], []
+    for k in range(H + 1):
+        rec_x.append(np.diag(Sig).copy())
+        rec_u.append(np.diag(K @ Sig @ K.T).copy())
+        if k < H:
+            Sig = Acl @ Sig @ Acl.T + Bd @ np.diag(d[k]) @ Bd.T
+    # gain table (the host side of gpmpc_set_tightening) and the convolution (the kernel)
+    tab, Am = [], np.eye(s.nx)
+    for m in range(H):
+        tab.append(np.vstack([(Am @ Bd) ** 2, (K @ Am @ Bd) ** 2]))   # [nb][n_unc]
+        Am = Acl @ Am
+    for k in range(H + 1):
+        sv = sum((tab[m] @ d[k - 1 - m] for m in range(k)), np.zeros(s.nx + s.nu))
+        np.testing.assert_allclose(sv[:s.nx], rec_x[k], rtol=1e-12, atol=1e-18)
+        np.testing.assert_allclose(sv[s.nx:], rec_u[k], rtol=1e-12, atol=1e-18)
