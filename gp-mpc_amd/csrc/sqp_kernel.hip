@@ -2,19 +2,25 @@
 //
 // One launch = one call of GPMPC.select_action for B instances (gpmpc/gpmpc.py:334-368):
 //   1. constraint tightening from the previous solution      (gpmpc/gpmpc.py:425-498)
-//      -- the GP variances come from gp_var_kernel (gp_kernels.hip)
+//      -- the GP variances come from gp_var_tri_kernel / gp_post_kernel (gp_kernels.hip); the
+//         H-step covariance recursion is evaluated as a convolution of the per-stage GP noise
+//         with a host-built gain table (ProblemDev::tgain), every stage in parallel
 //   2. acados-style SQP, Gauss-Newton Hessian, full steps,   (gpmpc/gpmpc.py:257-264)
 //      status codes 0/1/2/4 (gpmpc/gpmpc.py:365)
 //      a. linearisation: RK4 of prior + GP residual, exact tangent map (gpmpc/gpmpc.py:166-221)
-//         -- GP mean + gradient sums over the training set, split over lane chunks
+//         -- GP mean + input-gradient sums over the training set as MFMA tile contractions
+//            (gp_tiles: exponents on v_mfma_f64_16x16x4, sums on v_mfma_f64_4x4x4_4b)
 //      b. NLP residuals (stat / eq / ineq / comp) with the previous multipliers
 //      c. box-constrained LQ sub-problem: Mehrotra primal-dual IPM whose Newton systems
-//         are solved by a Riccati recursion over the horizon (the HPIPM structure)
+//         are solved by a Riccati recursion over the horizon (the HPIPM structure): the
+//         factorisation on MFMA (mfma_backward) when a stage fits a 16x16 tile, the VALU
+//         otherwise; forward and corrector sweeps on the VALU with readlane broadcasts
 //   3. u0, the new iterate (= x_prev/u_prev for the next step) and the multipliers.
 //
-// Lane layout: lane k (0..H) owns stage k: w_k = [x_k; u_k] (x_0 fixed to obs, u_H absent),
-// its bounds, IPM slacks/multipliers and the dynamics multiplier pi_k.  The Riccati
-// recursion is sequential over stages and parallel over matrix entries (lanes).
+// Lane layout: lane k (0..H) owns stage k for the SQP-level work: w_k = [x_k; u_k] (x_0 fixed to
+// obs, u_H absent), its bounds and the dynamics multiplier pi_k.  The IPM state of a stage is
+// split over lanes k and k + 32 when H + 1 <= 32 (SPL).  The Riccati recursion is sequential
+// over stages and parallel over matrix entries.  DESIGN.md §2.1 has the layouts and timings.
 #include <type_traits>
 
 #include "gpmpc_common.h"
