@@ -286,3 +286,30 @@ def test_tightening_convolution_matches_recursion(name):
         sv = sum((tab[m] @ d[k - 1 - m] for m in range(k)), np.zeros(s.nx + s.nu))
         np.testing.assert_allclose(sv[:s.nx], rec_x[k], rtol=1e-12, atol=1e-18)
         np.testing.assert_allclose(sv[s.nx:], rec_u[k], rtol=1e-12, atol=1e-18)
+
+
+def test_product_path_fails_loudly_without_gpu_or_library():
+    """No CPU fallback anywhere on the product path: without a HIP device the GP posterior and the
+    batched solver raise GPMPCError, and a missing library is reported as such (fresh process, so
+    the loader's module state is clean)."""
+    import subprocess
+    import sys
+    import torch
+
+    from gpmpc import _lib
+    from gpmpc.gp import GaussianProcess
+    from gpmpc.solver import BatchSolver
+
+    if torch.cuda.is_available():
+        pytest.skip("checks the no-GPU behaviour")
+    gp = GaussianProcess(torch.rand(8, 1, dtype=torch.float64), torch.rand(8, dtype=torch.float64))
+    with pytest.raises(_lib.GPMPCError):
+        gp.predict(torch.rand(4, 1, dtype=torch.float64))
+    with pytest.raises(_lib.GPMPCError):
+        BatchSolver(get_spec("quad2d"), 30, 4, device="cpu")
+    code = ("import sys; sys.path.insert(0, 'gp-mpc_amd'); from gpmpc import _lib\n"
+            "try:\n    _lib.load(require_gpu=False)\nexcept _lib.GPMPCError as e:\n    print('ERR', e)\n")
+    root = Path(__file__).resolve().parents[1]
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120,
+                         env={**__import__("os").environ, "GPMPC_LIB": "/nonexistent/libgpmpc_mi355x.so"})
+    assert "ERR HIP extension not built" in out.stdout, out.stdout + out.stderr
