@@ -1015,15 +1015,29 @@ struct SqpKernel {
                 }
             }
         } else {
-#pragma unroll 4
-            for (int e = lane; e < H * NX; e += 64) {
-                const int k = e / NX, i = e - k * NX;
-                const double* G = L.G + (size_t)k * NX * GS + i * GS;
-                const double* Kk = L.K + (size_t)k * NU * PS;
-                double acc = G[NB];
+            // three entries per pass, all computed before any is stored (the stores to A' would
+            // otherwise order the next entry's reads behind them)
+            const int n = H * NX;
+            for (int e0 = lane; e0 < n; e0 += 192) {
+                double acc[3];
 #pragma unroll
-                for (int a = 0; a < NU; ++a) acc = fma(G[NX + a], Kk[a * PS + NX], acc);
-                L.Acl[(size_t)k * NX * PS + i * PS + NX] = acc;
+                for (int r = 0; r < 3; ++r) {
+                    const int e = min(e0 + 64 * r, n - 1);
+                    const int k = e / NX, i = e - k * NX;
+                    const double* G = L.G + (size_t)k * NX * GS + i * GS;
+                    const double* Kk = L.K + (size_t)k * NU * PS;
+                    acc[r] = G[NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc[r] = fma(G[NX + a], Kk[a * PS + NX], acc[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const int e = e0 + 64 * r;
+                    if (e < n) {
+                        const int k = e / NX, i = e - k * NX;
+                        L.Acl[(size_t)k * NX * PS + i * PS + NX] = acc[r];
+                    }
+                }
             }
         }
     }
@@ -1107,17 +1121,27 @@ struct SqpKernel {
     __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
-        for (int e = lane; e < H * NX; e += 64) {
+        // entries (k, i) two per pass, both computed before either is stored (T and VT alias other
+        // LDS buffers, so a store would otherwise order the next entry's reads behind it)
+        const int n = H * NX;
+        auto t_entry = [&](int e) {
             const int k = e / NX, i = e - k * NX;
             const double* Pn = L.P + (size_t)(k + 1) * PP;
             const double* G = L.G + (size_t)k * NX * GS;
             double acc = 0.0;
 #pragma unroll
             for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
-            T[e] = acc;
+            return acc;
+        };
+        for (int e0 = lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            T[e0] = a0;
+            if (has1) T[e1] = a1;
         }
         WSYNC();
-        for (int e = lane; e < H * NX; e += 64) {
+        auto vt_entry = [&](int e) {
             const int k = e / NX, i = e - k * NX;
             const double* A = L.Acl + (size_t)k * NX * PS;
             const double* Kk = L.K + (size_t)k * NU * PS;
@@ -1126,7 +1150,14 @@ struct SqpKernel {
             for (int a = 0; a < NU; ++a) acc = fma(Kk[a * PS + i], L.gq[k * NB + NX + a], acc);
 #pragma unroll
             for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
-            VT[e] = acc;
+            return acc;
+        };
+        for (int e0 = lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = vt_entry(e0), a1 = vt_entry(has1 ? e1 : e0);
+            VT[e0] = a0;
+            if (has1) VT[e1] = a1;
         }
         WSYNC();
         const int col = lane < NX ? lane : 0;
