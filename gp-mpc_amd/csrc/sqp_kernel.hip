@@ -1249,7 +1249,7 @@ struct SqpKernel {
     __device__ static void ctpi(const Lds& L, int H, int lane, const double (&pi)[NX], double (&out)[NB]) {
         double pim1[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pim1[i] = __shfl(pi[i], lane > 0 ? lane - 1 : 0);
+        for (int i = 0; i < NX; ++i) pim1[i] = dpp_d<0x138>(pi[i]);   // wave_shr:1, lane - 1 (lane 0: unused)
         const double* G = L.G + (size_t)min(lane, H - 1) * NX * GS;
         double g[NX][NB];
 #pragma unroll
@@ -1290,10 +1290,9 @@ struct SqpKernel {
     // C' pi restricted to this lane's variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
     template <bool SPL, int NV>
     __device__ static void ctpi_q(const Lds& L, int H, int kq, int vb, const double (&pi)[NX], double (&out)[NV]) {
-        const int lane = threadIdx.x;
         double pim1[NX];   // pi of stage kq - 1: the previous lane of the same half
 #pragma unroll
-        for (int i = 0; i < NX; ++i) pim1[i] = __shfl(pi[i], lane > 0 ? lane - 1 : 0);
+        for (int i = 0; i < NX; ++i) pim1[i] = dpp_d<0x138>(pi[i]);   // wave_shr:1, lane - 1 (lane 0: unused)
         const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS + vb;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
@@ -1315,12 +1314,18 @@ struct SqpKernel {
     __device__ static void dyn_residual_q(const Lds& L, int H, int kq, const double (&d)[NV], const double (&c)[NX],
                                           double (&r)[NX]) {
         const int lane = threadIdx.x;
-        double df[NB], xn[NX];   // full stage vectors of stages kq and kq + 1
+        // full stage vectors of stages kq and kq + 1, by lane moves without the LDS crossbar: the
+        // other half of the stage is lane ^ 32 (permlane32 swap), the next stage is lane + 1 of the
+        // same half (DPP wave_shl:1; lanes whose source is past the end are unused stages)
+        double df[NB], xn[NX];
+        const int h = lane >> 5;
+        double dother[NV];
 #pragma unroll
-        for (int v = 0; v < NB; ++v) df[v] = SPL ? __shfl(d[v % NV], kq + 32 * (v / NV)) : d[v % NV];
+        for (int j = 0; j < NV; ++j) dother[j] = SPL ? xor32_d(d[j]) : d[j];
 #pragma unroll
-        for (int i = 0; i < NX; ++i)
-            xn[i] = SPL ? __shfl(d[i % NV], min(kq + 1 + 32 * (i / NV), 63)) : __shfl(d[i % NV], lane < 63 ? lane + 1 : 63);
+        for (int v = 0; v < NB; ++v) df[v] = (!SPL || v / NV == h) ? d[v % NV] : dother[v % NV];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) xn[i] = dpp_d<0x130>((!SPL || i / NV == h) ? d[i % NV] : dother[i % NV]);
         const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
