@@ -1514,7 +1514,7 @@ struct SqpKernel {
             ctpi(L, H, lane, pi, ct);
             double xn[NX];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) xn[i] = __shfl(w[i], lane < 63 ? lane + 1 : 63);
+            for (int i = 0; i < NX; ++i) xn[i] = dpp_d<0x130>(w[i]);   // wave_shl:1, stage k + 1 (lane 63 unused)
             double r_stat = 0.0, r_eq = 0.0, r_ineq = 0.0, r_comp = 0.0;
             double g[NB];
 #pragma unroll
@@ -1557,7 +1557,7 @@ struct SqpKernel {
             auto qv = [&](const double (&full)[NB], int j) {
                 const double lo = (j < NB) ? full[j < NB ? j : 0] : 0.0;
                 if constexpr (!SPL) return lo;
-                const double up = __shfl((NV + j < NB) ? full[NV + j < NB ? NV + j : 0] : 0.0, kq);
+                const double up = xor32_d((NV + j < NB) ? full[NV + j < NB ? NV + j : 0] : 0.0);   // lane kq
                 return hi_half ? up : lo;
             };
             double blo[NV], bup[NV], gv[NV], hd[NV], d[NV], sl[NV], su[NV], ll[NV], lu[NV], piq[NX], cqq[NX];
@@ -1587,7 +1587,12 @@ struct SqpKernel {
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
                 piq[i] = 0.0;
-                cqq[i] = SPL ? __shfl(cq[i], kq) : cq[i];
+                if constexpr (SPL) {
+                    const double o = xor32_d(cq[i]);   // lane kq for the upper half
+                    cqq[i] = hi_half ? o : cq[i];
+                } else {
+                    cqq[i] = cq[i];
+                }
             }
             bool qp_ok = true;
             int qit = 0;
@@ -1776,7 +1781,7 @@ struct SqpKernel {
                 // d of variable v of this lane's stage (lane = stage layout: lanes 0..31)
                 double dv = (v < NV) ? d[v < NV ? v : 0] : 0.0;
                 if constexpr (SPL) {
-                    const double up = __shfl(d[v >= NV ? v - NV : 0], lane + 32 < 64 ? lane + 32 : lane);
+                    const double up = xor32_d(d[v >= NV ? v - NV : 0]);   // lane + 32 (upper lanes: unused)
                     dv = (v >= NV) ? up : dv;
                 }
                 const bool av = v < NX ? (act_x || lane == 0) : act_u;
