@@ -11,6 +11,10 @@ sharded by rank, no collective in the data path; barrier + max-over-ranks timing
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+``--gpus N`` without torchrun launches the N ranks itself (gpmpc/launch.py, before any GPU
+call).  ``--dry-run`` replaces the GPU step by a rank-dependent host sleep: it exercises the
+launcher, the instance shards and the max-over-ranks timing on the CPU (gloo), for tests.
 """
 
 from __future__ import annotations
@@ -27,10 +31,15 @@ sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
 sys.path.insert(0, str(ROOT))
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
+
+from gpmpc.launch import maybe_spawn, rank_env  # noqa: E402  (no GPU/torch.cuda use)
 
 METRIC = "GP-MPC control steps/sec, 2D quadrotor H=30 N=200, batch 1024 @1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 dense peak (vector and matrix are equal on gfx950)
+# exp_rbf (csrc/gpmpc_common.h) is 15 f64 VALU operations + 2 integer ones: the VALU ceiling of
+# exps is the FP64 FMA-lane rate (78.6 TFLOP/s / 2) over 17 issued instructions
+EXP_VALU_OPS = 17
+EXP_CEILING_PER_S = FP64_PEAK_TFLOPS * 1e12 / 2 / EXP_VALU_OPS
 
 
 def gp_flops(spec, n_train, H):
@@ -61,12 +70,12 @@ def cpu_threads() -> int:
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats):
+def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, fitc=None, heavy=False):
     """Time the C++ CPU restatement (oracle/cpu_ref.cpp: SQP-GN + Mehrotra IPM with Riccati
     Newton steps, OpenMP over instances) on a bounded closed-loop sample of the same workload:
-    all host cores over a batch of 4 instances per thread (value), and one instance on one core
-    (the reference's usage pattern).  The first, cold step of each run is not timed
-    (gpmpc/plotting.py:25)."""
+    all host cores over a batch of instances (value; 4 per thread, 1 per thread for heavy
+    workloads), and one instance on one core (the reference's usage pattern).  The first, cold
+    step of each run is not timed (gpmpc/plotting.py:25)."""
     from oracle import cpu_ref
     from oracle import gpmpc_oracle as O
     from gpmpc.synthetic import initial_states
@@ -76,10 +85,10 @@ def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats):
     traj = spec.reference_trajectory()
 
     def run(B, threads, budget):
-        ref = cpu_ref.CpuRef(spec, H, B, gps=gps, lqr_mats=lqr_mats)
+        ref = cpu_ref.CpuRef(spec, H, B, gps=gps, lqr_mats=lqr_mats, fitc=fitc)
         x0, phase = initial_states(spec, traj, B)
         steps, elapsed, k = 0, 0.0, 0
-        while elapsed < budget or steps < 2:
+        while elapsed < budget or steps < 1:
             t0 = time.perf_counter()
             u0 = ref.step(x0, phase + k, threads=threads)
             dt = time.perf_counter() - t0
@@ -92,18 +101,18 @@ def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats):
         return B * steps / elapsed, steps, ref
 
     threads = cpu_threads()
-    Bc = 4 * threads
+    Bc = (1 if heavy else 4) * threads
     v_all, n_all, ref = run(Bc, threads, 0.65 * seconds)
     v_one, n_one, _ = run(1, 1, 0.35 * seconds)
     return {"value": float(v_all), "unit": "control steps/s", "cores": threads, "kind": "port",
             "single_instance_1core": float(v_one),
-            "sample": f"C++ restatement (oracle/cpu_ref.cpp, -O3 AVX2, OpenMP), {spec.name} N={data[0][0].shape[0]} "
-                      f"H={H} exact GP: {Bc} instances x {n_all} closed-loop steps on {threads} threads; "
-                      f"single_instance_1core: 1 instance x {n_one} steps on 1 thread; first step of each run "
-                      f"untimed; sqp_iter mean {float(ref.sqp_iter.mean()):.2f}"}
+            "sample": f"C++ restatement (oracle/cpu_ref.cpp, -O3 AVX2, OpenMP), {spec.name} N={data[0][0].shape[0]}"
+                      f"{' FITC M=%d' % len(fitc[0][1]) if fitc else ''} H={H}: {Bc} instances x {n_all} closed-loop "
+                      f"steps on {threads} threads; single_instance_1core: 1 instance x {n_one} steps on 1 thread; "
+                      f"first step of each run untimed; sqp_iter mean {float(ref.sqp_iter.mean()):.2f}"}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -121,25 +130,91 @@ def main():
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
     ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
                     help="tools/pmc_summary.py output of the same command (roofline.traffic)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal: host sleep instead of the GPU step (launcher / shards / timing)")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+def workload_name(spec, args):
+    N, H, B = args.n_train, args.horizon, args.batch
+    return (f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}"
+            f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}, "
+            f"{B} instances per GPU, closed loop")
+
+
+def init_dist(world, gpu, use_gpu):
+    """torch.distributed process group (RCCL by default, GPMPC_DIST_BACKEND=gloo to rehearse)."""
+    if world <= 1:
+        return None
+    import torch
+    import torch.distributed as dist
+
+    backend = os.environ.get("GPMPC_DIST_BACKEND", "nccl" if use_gpu else "gloo")   # nccl = RCCL on ROCm
+    if backend == "nccl":
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", gpu))
+    else:
+        dist.init_process_group(backend=backend)
+    return dist
+
+
+def reduce_timing(dist, elapsed, extra, dev=None):
+    """Max over ranks of [elapsed, *extra] (the slowest rank sets the job's time)."""
+    import torch
+
+    t = torch.tensor([elapsed, *extra], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
+def run_dry(args, rank, world):
+    """CPU rehearsal of the multi-rank bench: the same shards, barriers and max-over-ranks
+    timing around a host sleep of (1 + rank) ms per step."""
+    from gpmpc import distributed as D
+    from gpmpc.models import get_spec
+
+    dist = init_dist(world, 0, use_gpu=False)
+    spec = get_spec(args.model)
+    ids = D.shard_range(args.batch, rank)
+    for _ in range(args.warmup):
+        time.sleep(1e-3 * (1 + rank))
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(1e-3 * (1 + rank))
+    local = time.perf_counter() - t0   # this rank's own work, before the closing barrier
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed, = reduce_timing(dist, elapsed, [])
+    shards = [None] * world
+    if dist is not None:
+        dist.all_gather_object(shards, [ids.start, ids.stop, local])
+    else:
+        shards = [[ids.start, ids.stop, local]]
+    if rank == 0:
+        total = args.batch * world
+        print(json.dumps({"metric": METRIC, "value": total * args.steps / elapsed, "unit": "control steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "f64", "data": "dry run (host sleep, no GPU)",
+                          "config": {"workload": workload_name(spec, args), "model": spec.name,
+                                     "global_batch": total, "horizon": args.horizon, "n_train": args.n_train,
+                                     "parallelism": f"instances sharded over {world} rank(s)"},
+                          "shards": shards}))
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_gpu(args, rank, local_rank, world):
+    import torch
+
     # one rank per GPU (local_rank modulo the visible GPUs only matters for a rehearsal of the
     # multi-rank path on fewer GPUs, with GPMPC_DIST_BACKEND=gloo)
     gpu = local_rank % max(torch.cuda.device_count(), 1)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        backend = os.environ.get("GPMPC_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
-        if backend == "nccl":
-            dist.init_process_group(backend="nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(backend=backend)
+    dist = init_dist(world, gpu, use_gpu=True)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
@@ -183,7 +258,7 @@ def main():
     x0_all, phase_all = initial_states(spec, traj, B * world, seed=1)
     obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
     tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
-    stats_buf = torch.zeros(B, 8, dtype=torch.int64, device=dev)   # accumulated inside the SQP kernel
+    stats_buf = torch.zeros(B, BatchSolver.STATS_SLOTS, dtype=torch.int64, device=dev)   # filled by the SQP kernel
     solver.set_stats(stats_buf)
 
     def step():
@@ -194,7 +269,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    solver.kernel_times()  # drop warm-up events
+    solver.kernel_time_list()  # drop warm-up events
     stats_buf.zero_()
     torch.cuda.synchronize(dev)
     if dist is not None:
@@ -208,16 +283,16 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     solver.set_profiling(False)
-    kt = solver.kernel_times()
-    stats = torch.tensor([elapsed, kt["sqp_ms"], kt["var_ms"]], dtype=torch.float64, device=dev)
+    kt = solver.kernel_time_list()
+    sqp_list, var_list = kt["sqp_ms"], kt["var_ms"]
+    elapsed, sqp_sum, var_sum = reduce_timing(dist, elapsed, [sum(sqp_list), sum(var_list)], dev)
     tot = stats_buf.sum(0).to(torch.float64)
-    sums = tot[:2].clone()
-    status_counts = tot[2:7].clone()
+    mx = stats_buf.max(0).values.to(torch.float64)
+    sums, status_counts, maxes = tot[:2].clone(), tot[2:7].clone(), mx[7:9].clone()
     if dist is not None:
-        dist.all_reduce(stats, op=dist.ReduceOp.MAX)
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
-    elapsed = float(stats[0])
+        dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
     total_instances = B * world
     value = total_instances * args.steps / elapsed
     sqp_mean = float(sums[0]) / (total_instances * args.steps)
@@ -226,15 +301,14 @@ def main():
     if rank == 0:
         per_lin, exps_lin, var_flops = gp_flops(spec, N, H)
         # dominant kernel: the SQP kernel; linearisations per instance-step = sqp_iter + 1
-        sqp_ms = float(stats[1]) / max(kt["sqp_launches"], 1)
+        sqp_ms = sqp_sum / max(len(sqp_list), 1)
         flops_sqp = B * (sqp_mean + 1.0) * per_lin          # per launch (one rank's batch)
         achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
-        var_ms = float(stats[2]) / max(kt["var_launches"], 1)
-        var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if kt["var_launches"] else None
-        workload = f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}" \
-                   f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}, " \
-                   f"{B} instances per GPU, closed loop"
-        traffic = None
+        var_ms = var_sum / max(len(var_list), 1)
+        var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if var_list else None
+        exps_launch = B * (sqp_mean + 1.0) * exps_lin
+        workload = workload_name(spec, args)
+        traffic, traffic_src = None, None
         try:
             with open(args.pmc_summary) as fh:
                 pmc = json.load(fh)
@@ -242,11 +316,16 @@ def main():
                 pre = "gpmpc::sqp_step_kernel<%d" % spec.model_id   # <ID> or <ID, split-layout flag>
                 e = next((v for kname, v in pmc["kernels"].items() if kname.startswith(pre)), {})
                 traffic = e.get("hbm_bytes_est")
+                if traffic is not None:
+                    traffic_src = (f"{os.path.relpath(args.pmc_summary, ROOT)} (rocprofv3 FETCH_SIZE / WRITE_SIZE passes "
+                                   f"of this command, committed; 2 x FETCH + WRITE per launch)")
         except (OSError, ValueError, KeyError):
             traffic = None
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not args.fitc:   # rank 0 at N=1 only
-            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats)
+        if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
+            heavy = args.fitc > 0 or N >= 2000
+            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, fitc=fitc, heavy=heavy)
+        sq = np.array(sqp_list) if sqp_list else np.zeros(1)
         out = {
             "metric": METRIC,
             "value": value,
@@ -265,7 +344,7 @@ def main():
                        "parallelism": f"instances sharded over {world} GPU(s), GP replicated"},
             "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "note": "FP64 GP mean+gradient contraction flops / HIP-event kernel time; peak = FP64 "
                                  "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
                                  "Riccati recursion"},
@@ -274,18 +353,42 @@ def main():
                            else "gp_post_kernel<true>"),
                 "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},
+            "exp_ceiling": {"exps_per_launch": exps_launch, "achieved_per_s": exps_launch / (sqp_ms * 1e-3),
+                            "ceiling_per_s": EXP_CEILING_PER_S,
+                            "frac": exps_launch / (sqp_ms * 1e-3) / EXP_CEILING_PER_S,
+                            "note": f"GP-phase exps over the whole SQP-kernel time; ceiling = FP64 VALU FMA-lane "
+                                    f"rate / {EXP_VALU_OPS} instructions per exp_rbf"},
             "kernel_ms_per_step": {"sqp": sqp_ms, "variance": var_ms},
+            "sqp_kernel_ms_per_step_distribution": {
+                "min": float(sq.min()), "p50": float(np.median(sq)), "p90": float(np.percentile(sq, 90)),
+                "max": float(sq.max()), "per_step": [round(float(v), 4) for v in sq]},
             "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
             "sqp_iter_mean": sqp_mean,
+            "sqp_iter_max": int(maxes[0]),
             "qp_iter_mean_per_step": qp_mean,
+            "qp_iter_max_per_step": int(maxes[1]),
             "status_counts": {str(i): int(status_counts[i]) for i in range(5)},
-            "exps_per_sqp_launch": B * (sqp_mean + 1.0) * exps_lin,
+            "exps_per_sqp_launch": exps_launch,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    # N ranks without torchrun: relaunch under torch.distributed.run before touching the GPU
+    maybe_spawn(args.gpus, str(Path(__file__).resolve()), argv)
+    rank, local_rank, world = rank_env()
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if args.dry_run:
+        run_dry(args, rank, world)
+    else:
+        run_gpu(args, rank, local_rank, world)
 
 
 if __name__ == "__main__":

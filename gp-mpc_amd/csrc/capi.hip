@@ -548,6 +548,31 @@ gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var,
     return sum(h->ev_sqp, sqp_ms, n_sqp);
 }
 
+gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms, int32_t* n_var, double* sqp_ms,
+                                    int32_t* n_sqp) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (cap < 0) return fail(GPMPC_ERR_ARG, "negative capacity");
+    (void)hipSetDevice(h->device);
+    auto take = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
+        int32_t i = 0;
+        for (auto& pr : v) {
+            HIPCHK(hipEventSynchronize(pr.second));
+            float t = 0.0f;
+            HIPCHK(hipEventElapsedTime(&t, pr.first, pr.second));
+            if (ms && i < cap) ms[i] = t;
+            ++i;
+            h->ev_pool.push_back(pr.first);
+            h->ev_pool.push_back(pr.second);
+        }
+        if (n) *n = i;
+        v.clear();
+        return GPMPC_OK;
+    };
+    gpmpc_status st = take(h->ev_var, var_ms, n_var);
+    if (st != GPMPC_OK) return st;
+    return take(h->ev_sqp, sqp_ms, n_sqp);
+}
+
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     h->timing = (unsigned long long*)timing_dev;

@@ -12,6 +12,7 @@ constexpr int kMaxNU = 4;
 constexpr int kMaxH = 63;       // one lane per stage 0..H (64-lane wavefront)
 constexpr int kPhases = 12;  // diagnostic phase slots (GPMPC_TIMING builds)
 constexpr int kMaxParams = 16;
+constexpr int kStatsSlots = 10;  // per-instance solver statistics (gpmpc_set_stats_buffer)
 
 enum ModelId : int32_t { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };
 
@@ -49,7 +50,7 @@ struct ProblemDev {
     int32_t use_gp;           // 0: nominal MPC (gpmpc/mpc.py)
     double dt;
     double cost_scale;        // acados cost_scaling for stages 0..H-1 (time step), 1 for terminal
-    double uh;                // h <= uh: -1e-8 GPMPC (gpmpc.py:309-314), +1e-8 MPC (mpc.py:242-247)
+    double uh;                // h <= uh: -1e-8 GPMPC (gpmpc.py:309-314), +1e-8 MPC (mpc.py:157-162)
     double params[kMaxParams];
     double x_lo[kMaxNX], x_hi[kMaxNX], u_lo[kMaxNU], u_hi[kMaxNU];
     double q[kMaxNX], r[kMaxNU], u_eq[kMaxNU];
@@ -91,7 +92,8 @@ struct StepIO {
     int32_t* qp_iter;        // [B] out, total IPM iterations
     double* res;             // [B][4] out, final NLP residuals (stat, eq, ineq, comp)
     unsigned long long* timing;  // [B][kPhases] phase cycles (GPMPC_TIMING builds only), may be null
-    long long* stats;            // [B][8] running sums: sqp iters, qp iters, status 0..4 counts; may be null
+    long long* stats;            // [B][kStatsSlots] sqp iters, qp iters (sums), status 0..4 counts,
+                                 // max sqp iters, max qp iters per solve; may be null
 };
 
 // Arguments of the GP posterior kernel (gp_kernels.hip).

@@ -1479,11 +1479,24 @@ struct SqpKernel {
         auto ubv = [&](int v) { return (v < NX ? P.x_hi[v] : P.u_hi[v - NX]) - tsd[v] + P.uh; };
 
         [[maybe_unused]] const Entries E = decode(lane);
+        // ---------------- stage-0 state rows (gpmpc.py:288,296,309-310; mpc.py:141,145,157-158)
+        // x_0 is pinned to obs (lbx = ubx = obs, gpmpc.py:339-340), so these rows only decide
+        // feasibility: an obs outside the stage-0 box by more than the inequality tolerance makes
+        // every QP infeasible, which acados reports as a QP failure (status 4; the reference then
+        // asserts, gpmpc.py:365).  Within the tolerance the rows enter the NLP residual only.
+        double v0 = 0.0;   // largest stage-0 state-row violation of x0 (NaN-propagating)
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const double e = fmax(P.x_lo[i] - P.uh - x0[i], x0[i] - P.x_hi[i] - P.uh);
+            v0 = (e == e && v0 == v0) ? fmax(v0, e) : __builtin_nan("");
+        }
+        const bool x0_ok = v0 <= P.tol_ineq;   // uniform: x0 and the bounds are the same on every lane
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
         const double nc = 2.0 * (double)H * (double)NB;
         int status = kMaxIter, it = 0, qp_total = 0;
         double res[4] = {0, 0, 0, 0};
-        for (it = 0;; ++it) {
+        if (!x0_ok) status = kQPFailure;
+        for (it = 0; x0_ok; ++it) {
             double lamL[NB], lamU[NB], pi[NX];
 #pragma unroll
             for (int v = 0; v < NB; ++v) {
@@ -1536,7 +1549,11 @@ struct SqpKernel {
             }
             if (lane == 0) {
 #pragma unroll
-                for (int i = 0; i < NX; ++i) r_ineq = fmax(r_ineq, fabs(x0[i] - w[i]));  // lbx = ubx = obs
+                for (int i = 0; i < NX; ++i) {
+                    r_ineq = fmax(r_ineq, fabs(x0[i] - w[i]));  // lbx = ubx = obs
+                    // stage-0 state rows on the iterate's x_0 (= obs after the first step)
+                    r_ineq = fmax(r_ineq, fmax(P.x_lo[i] - P.uh - w[i], w[i] - P.x_hi[i] - P.uh));
+                }
             }
             res[0] = wave_max(r_stat);
             res[1] = wave_max(r_eq);
@@ -1806,28 +1823,46 @@ struct SqpKernel {
         // ---------------- write back (acados memory + x_prev/u_prev, gpmpc.py:366-368)
         double* xo = S.x + (size_t)b * (H + 1) * NX;
         double* uo = S.u + (size_t)b * H * NU;
-        if (on) {   // (the multipliers are already in S.lam / S.pi)
+        // A failed solve (status 1 or 4; the reference asserts on it, gpmpc.py:365) must not poison
+        // the instance's next step: the iterate keeps the previous solution, the multipliers
+        // restart from zero, u0 is the previous solution's first input and the next step runs
+        // untightened (as after a reset).
+        const bool good = (status == kSuccess) || (status == kMaxIter);
+        if (good) {   // (the multipliers are already in S.lam / S.pi)
+            if (on) {
 #pragma unroll
-            for (int i = 0; i < NX; ++i) xo[k * NX + i] = w[i];
-        }
-        if (act_u) {
+                for (int i = 0; i < NX; ++i) xo[k * NX + i] = w[i];
+            }
+            if (act_u) {
 #pragma unroll
-            for (int a = 0; a < NU; ++a) uo[k * NU + a] = w[NX + a];
+                for (int a = 0; a < NU; ++a) uo[k * NU + a] = w[NX + a];
+            }
+        } else {
+            if (on) {
+#pragma unroll
+                for (int v = 0; v < 2 * NB; ++v) lam_g[v] = 0.0;
+            }
+            if (act_u) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pi_g[i] = 0.0;
+            }
         }
         if (lane == 0) {
 #pragma unroll
-            for (int a = 0; a < NU; ++a) io.u0[(size_t)b * NU + a] = w[NX + a];
+            for (int a = 0; a < NU; ++a) io.u0[(size_t)b * NU + a] = good ? w[NX + a] : uo[a];
             io.status[b] = status;
             io.sqp_iter[b] = it;
             io.qp_iter[b] = qp_total;
 #pragma unroll
             for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
-            S.has_prev[b] = 1;
+            S.has_prev[b] = good ? 1 : 0;
             if (io.stats != nullptr) {
-                long long* st = io.stats + (size_t)b * 8;
+                long long* st = io.stats + (size_t)b * kStatsSlots;
                 st[0] += it;
                 st[1] += qp_total;
                 if (status >= 0 && status <= 4) st[2 + status] += 1;
+                st[7] = max(st[7], (long long)it);
+                st[8] = max(st[8], (long long)qp_total);
             }
         }
     }

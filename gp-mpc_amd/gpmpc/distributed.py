@@ -44,6 +44,56 @@ def replicate_training_data(data: list[tuple[np.ndarray, np.ndarray]], device=No
     return out
 
 
+def _coll_device():
+    """Device of collective buffers: the current GPU for RCCL ("nccl"), the host for gloo."""
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def gather_rows(a: np.ndarray) -> np.ndarray:
+    """All-gather the rows of a 2-D array from every rank, concatenated in rank order (the same
+    result on every rank).  Used once per learning epoch for the newly sampled transitions
+    (the reference's single process stacks them at
+    `scripts/run_gp_mpc.py:115-118`).  Row counts may differ between ranks."""
+    a = np.ascontiguousarray(np.atleast_2d(np.asarray(a, dtype=np.float64)))
+    rank, size = world()
+    if size == 1:
+        return a
+    dev = _coll_device()
+    n = torch.tensor([a.shape[0]], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(size)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts)
+    buf = torch.zeros((m, a.shape[1]), dtype=torch.float64, device=dev)
+    buf[: a.shape[0]] = torch.as_tensor(a, device=dev)
+    parts = [torch.zeros_like(buf) for _ in range(size)]
+    dist.all_gather(parts, buf)
+    return np.concatenate([p[:c].cpu().numpy() for p, c in zip(parts, counts)], axis=0)
+
+
+def assert_replicated(*arrays) -> None:
+    """Raise if the arrays differ between ranks (order-sensitive checksum, max vs min over ranks).
+    The data-parallel GP fit sums gradient row-slices and is only valid on identical data."""
+    rank, size = world()
+    if size == 1:
+        return
+    sig = []
+    for a in arrays:
+        v = np.asarray(a, dtype=np.float64).ravel()
+        w = np.arange(1, v.size + 1, dtype=np.float64)
+        sig += [float(v.size), float(v.sum()), float((w * v).sum()), float((v * v).sum())]
+    dev = _coll_device()
+    hi = torch.tensor(sig, dtype=torch.float64, device=dev)
+    lo = -hi.clone()
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    dist.all_reduce(lo, op=dist.ReduceOp.MAX)
+    if not torch.equal(hi, -lo):
+        raise RuntimeError("GP training data differs between ranks: the data-parallel fit needs identical "
+                           "replicas (gather the transitions with gather_rows first)")
+
+
 def max_over_ranks(values: list[float], device=None) -> list[float]:
     rank, size = world()
     if size == 1:

@@ -29,11 +29,14 @@ from .solver import BatchSolver, STATUS_NAMES, inverse_cdf, setup_prior_dynamics
 class GPMPC:
     """Implements a GP-MPC controller on the MI355X HIP solver."""
 
+    # the reference's quadrotor hover input (`gpmpc/gpmpc.py:18`); an instance's U_EQ is its model's
+    U_EQ: np.ndarray = np.array([0.3234, 0, 0, 0])
+
     def __init__(self, symbolic_model, traj: np.ndarray | None = None, prior_params: dict | None = None,
                  horizon: int = 25, q_mpc: list | None = None, r_mpc: list | None = None, sparse_gp: bool = False,
                  prob: float = 0.955, max_gp_samples: int = 30, seed: int = 1337, device: str = "cuda",
                  output_dir: Path | None = None, batch: int = 1, variance_inputs: str = "reference", **solver_kw):
-        spec = symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)
+        spec = (symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)).copy()
         # "reference": the variance input map of `gpmpc/gpmpc.py:437-444` (for quad3d it indexes the
         # full state-input vector with the GP-input-space indices); "dynamics": each GP's own inputs
         if variance_inputs == "dynamics":
@@ -57,8 +60,9 @@ class GPMPC:
         self.dt = spec.dt
         self.T = int(horizon)
         self.Q, self.R = np.diag(spec.q_diag), np.diag(spec.r_diag)
+        self.U_EQ = spec.u_eq.copy()
         self.traj = spec.reference_trajectory() if traj is None else np.asarray(traj, dtype=np.float64)
-        self.ref_action = np.repeat(spec.u_eq[:, None], self.T, axis=1)
+        self.ref_action = np.repeat(self.U_EQ[:, None], self.T, axis=1)
         self.traj_step = 0
         self.np_random = np.random.default_rng(seed)
         self.gp_idx = self._gp_columns(spec)
@@ -147,6 +151,8 @@ class GPMPC:
         from . import distributed as D
 
         _, size = D.world()
+        if size > 1:   # the row-split gradient of fit_gp_allreduce is only valid on identical replicas
+            D.assert_replicated(x, y)
         for i, idx in enumerate(self.gp_idx):
             gp = GaussianProcess(x_train[:, idx], y_train[:, i])
             if size > 1:   # data-parallel fit: one all-reduce of the MLL gradient per Adam step
@@ -199,7 +205,13 @@ class GPMPC:
                 fitc = self.precompute_sparse_posterior_mean(min(n, self.max_gp_samples))
             self.solver.set_gps(self.gaussian_process, with_variance=True, fitc=fitc)
             self._requires_recompile = False
-        self.solver.reset(reset_iterate=False)  # acados keeps its memory (gpmpc.py:94-111)
+            # new GPs: the reference builds a fresh AcadosOcpSolver (`gpmpc/gpmpc.py:97-108`), whose
+            # memory -- iterate and multipliers -- starts from zero
+            self.solver.reset(reset_iterate=True)
+        else:
+            # same GPs: acados keeps its memory across episodes (`gpmpc/gpmpc.py:94-111` does not
+            # reset the solver), so the first solve is warm-started from the last iterate
+            self.solver.reset(reset_iterate=False)
         self._x_prev = None
         self._u_prev = None
         self._has_prev = False

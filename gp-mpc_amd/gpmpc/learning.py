@@ -5,11 +5,13 @@ MPC, fits the GPs, and re-runs with GP-MPC each epoch.  Here an "environment" is
 synthetic plant kernel (``BatchSolver.plant_step``: RK4 of the model with its true
 parameters), so B episodes run at once on the GPU; transitions are gathered from all of them.
 
-* :func:`run_evaluation` -- one closed-loop episode per instance (`run_gp_mpc.py:42-75`)
-* :func:`sample_data`    -- random transitions of an episode batch (`run_gp_mpc.py:78-86`)
+* :func:`run_evaluation` -- one closed-loop episode per instance (`run_gp_mpc.py:42-72`)
+* :func:`sample_data`    -- random transitions of an episode batch (`run_gp_mpc.py:75-83`)
 * :func:`learn`          -- prior run, then per epoch: sample, ``preprocess_data``,
   ``train_gp`` (on the GPU; data-parallel under torch.distributed), ``reset``, test and
-  train episodes (`run_gp_mpc.py:89-137`)
+  train episodes (`run_gp_mpc.py:86-137`).  Under N ranks every rank runs its own contiguous
+  shard of the instances and the newly sampled transitions are all-gathered each epoch, so
+  every rank fits the same GPs on the same data.
 * :func:`get_runtime` / :func:`save_runtime_csv` -- the runtime summary and CSV of
   `gpmpc/plotting.py:10-62`.
 """
@@ -54,7 +56,7 @@ def run_evaluation(ctrl, x0: np.ndarray, steps: int, tstep0: np.ndarray | None =
 
 
 def sample_data(data: dict, n_samples: int, rng: np.random.Generator):
-    """Random transitions (x, u, x_next) from an episode batch (`scripts/run_gp_mpc.py:78-86`):
+    """Random transitions (x, u, x_next) from an episode batch (`scripts/run_gp_mpc.py:75-83`):
     the (step, instance) pairs are sampled without replacement."""
     steps, B = data["action"].shape[:2]
     n = steps * B
@@ -75,14 +77,19 @@ def tracking_cost(data: dict, traj: np.ndarray, tstep0: np.ndarray | None = None
 
 def learn(n_epochs: int, ctrl, lr: float, gp_iterations: int, seed: int, samples_per_epoch: int,
           episode_len: int, x0: np.ndarray | None = None, tstep0: np.ndarray | None = None):
-    """Episodic learning (`scripts/run_gp_mpc.py:89-137`): epoch 0 runs the prior MPC; every
+    """Episodic learning (`scripts/run_gp_mpc.py:86-137`): epoch 0 runs the prior MPC; every
     epoch then fits the GPs on all data gathered so far and runs a test and a train episode
     batch with GP-MPC.  Returns (train_runs, test_runs, timing) dicts keyed by epoch."""
+    from . import distributed as D
+
     spec = ctrl.model
-    rng = np.random.default_rng(seed)
+    rank, size = D.world()
+    rng = np.random.default_rng(seed if size == 1 else [seed, rank])
     B = ctrl.batch
-    if x0 is None:
-        x0, tstep0 = initial_states(spec, ctrl.traj, B, seed=seed)
+    if x0 is None:   # this rank's shard of the B * size instances
+        ids = D.shard_range(B, rank)
+        x0_all, t_all = initial_states(spec, ctrl.traj, B * size, seed=seed)
+        x0, tstep0 = x0_all[ids.start:ids.stop], t_all[ids.start:ids.stop]
     train_runs, test_runs, timing = {}, {}, {}
     plant = ctrl.solver
     train_runs[0] = run_evaluation(ctrl.prior_ctrl, x0, episode_len, tstep0, plant_solver=plant)
@@ -92,6 +99,8 @@ def learn(n_epochs: int, ctrl, lr: float, gp_iterations: int, seed: int, samples
     for epoch in range(1, n_epochs + 1):
         state, actions, next_state = sample_data(train_runs[epoch - 1], samples_per_epoch, rng)
         inputs, targets = ctrl.preprocess_data(state, actions, next_state)
+        # every rank's new transitions, in rank order (one all-gather per epoch)
+        inputs, targets = D.gather_rows(inputs), D.gather_rows(targets)
         x_train = np.vstack((x_train, inputs))
         y_train = np.vstack((y_train, targets))
         t3 = time.perf_counter()

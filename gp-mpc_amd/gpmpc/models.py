@@ -24,6 +24,7 @@ construction for the LQR gain (`gpmpc/gpmpc.py:81-86,500-507`).
 
 from __future__ import annotations
 
+import copy
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -219,6 +220,11 @@ class ModelSpec:
             traj[0] = 0.5 * np.sin(w * t)
             traj[1] = 0.5 * w * np.cos(w * t)
         return traj
+
+    def copy(self) -> "ModelSpec":
+        """Independent copy (controllers apply their q_mpc / r_mpc / prior_params to a copy, so the
+        caller's spec object is never mutated)."""
+        return copy.deepcopy(self)
 
     def to_dict(self) -> dict:
         """Plain-number view of the spec (what the CPU oracle consumes)."""

@@ -10,10 +10,10 @@ plots its single episode; here ``instance`` selects which of the B episodes is d
 * :func:`plot_runs`           -- one state over the epochs vs the reference (`plotting.py:65-86`)
 * :func:`plot_runs_input`     -- one input over the epochs (`plotting.py:89-104`)
 * :func:`plot_learning_curve` -- figure + CSV of a per-epoch scalar (`plotting.py:107-120`)
-* :func:`plot_path`           -- position paths in the model's planes (`plotting.py:123-158`,
+* :func:`plot_path`           -- position paths in the model's planes (`plotting.py:121-155`,
   generalised from the 3D quadrotor's x-y / x-z / y-z planes to quad2d's x-z and cartpole's x-theta)
-* :func:`make_plots`          -- the per-run figure set (`plotting.py:161-185`, ``make_quad_plots``)
-* :func:`plot_state_eval`     -- states vs reference over time (`plotting.py:188-228`)
+* :func:`make_plots`          -- the per-run figure set (`plotting.py:158-181`, ``make_quad_plots``)
+* :func:`plot_state_eval`     -- states vs reference over time (`plotting.py:184-228`)
 """
 
 from __future__ import annotations

@@ -161,10 +161,13 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_tightening(self._h, 1, inverse_cdf(prob, self.nx), Ad.ctypes.data,
                                                  Bd.ctypes.data, K.ctypes.data))
 
+    STATS_SLOTS = 10
+
     def set_stats(self, buf: torch.Tensor | None):
-        """Device int64 (B, 8) accumulator of SQP/QP iterations and status counts (or None)."""
+        """Device int64 (B, 10) accumulator of SQP/QP iteration sums, status counts and the
+        largest SQP / QP iteration counts of one solve (or None); see gpmpc_set_stats_buffer."""
         if buf is not None:
-            assert buf.shape == (self.batch, 8) and buf.dtype == torch.int64 and buf.device == self.device
+            assert buf.shape == (self.batch, self.STATS_SLOTS) and buf.dtype == torch.int64 and buf.device == self.device
         self._stats = buf
         _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr()))
 
@@ -178,6 +181,14 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_kernel_times(self._h, ctypes.byref(vm), ctypes.byref(vn), ctypes.byref(sm),
                                                ctypes.byref(sn)))
         return {"var_ms": vm.value, "var_launches": vn.value, "sqp_ms": sm.value, "sqp_launches": sn.value}
+
+    def kernel_time_list(self, cap: int = 4096) -> dict:
+        """Per-launch HIP-event milliseconds of the variance / SQP kernels since the last call."""
+        vm = (ctypes.c_double * cap)()
+        sm = (ctypes.c_double * cap)()
+        vn, sn = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.gpmpc_kernel_time_list(self._h, cap, vm, ctypes.byref(vn), sm, ctypes.byref(sn)))
+        return {"var_ms": list(vm[:min(vn.value, cap)]), "sqp_ms": list(sm[:min(sn.value, cap)])}
 
     # ------------------------------------------------------------------ stepping
     def _stream(self):

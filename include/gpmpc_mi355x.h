@@ -33,20 +33,24 @@ typedef enum {
 enum { GPMPC_MODEL_QUAD2D = 0, GPMPC_MODEL_QUAD3D = 1, GPMPC_MODEL_CARTPOLE = 2 };
 
 /* Per-instance solver status codes, identical to acados (asserted in {0,2} at
- * gpmpc/gpmpc.py:365 and gpmpc/mpc.py:270). */
+ * gpmpc/gpmpc.py:365 and gpmpc/mpc.py:185).  An obs outside the stage-0 state box
+ * (gpmpc/gpmpc.py:288,296,309-310; gpmpc/mpc.py:141,145,157-158) by more than the inequality
+ * tolerance makes the QP infeasible: GPMPC_QP_FAILURE, as acados reports it.  After a failed
+ * solve (NAN or QP_FAILURE) the instance keeps its previous iterate, its multipliers restart
+ * from zero and its next solve runs untightened (no poisoning of later steps). */
 enum { GPMPC_SUCCESS = 0, GPMPC_NAN = 1, GPMPC_MAXITER = 2, GPMPC_MINSTEP = 3, GPMPC_QP_FAILURE = 4 };
 
 /* Create a solver for `max_batch` independent instances of model `model_id` with horizon
  * `horizon` on HIP device `device`.
  * Replaces: AcadosOcpSolver(ocp, json) construction at gpmpc/gpmpc.py:105-107 and
- * gpmpc/mpc.py:143 (code generation + compile there; nothing to compile here). */
+ * gpmpc/mpc.py:58 (code generation + compile there; nothing to compile here). */
 gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, int32_t device, gpmpc_handle** out);
 void gpmpc_destroy(gpmpc_handle* h);
 const char* gpmpc_last_error(void);
 
 /* OCP definition (host arrays, float64).
  * Replaces: setup_acados_model / setup_acados_optimizer / setup_acados_constraints,
- * gpmpc/gpmpc.py:166-320 (and gpmpc/mpc.py:150-255).
+ * gpmpc/gpmpc.py:166-320 (and gpmpc/mpc.py:65-163).
  *   params      prior parameters in the model's order (gpmpc/models.py param_vector)
  *   x_lo..u_hi  box bounds (gpmpc/gpmpc.py:242-246)
  *   q_diag, r_diag  LINEAR_LS weights W = blkdiag(Q,R), W_e = Q (gpmpc/gpmpc.py:233-234)
@@ -100,7 +104,8 @@ gpmpc_status gpmpc_set_var_inputs(gpmpc_handle* h, int32_t gp_id, const int32_t*
 
 /* Forget the previous solution for instances [0, batch): the next solve runs without
  * tightening (GPMPC.reset, gpmpc/gpmpc.py:109-111).  reset_iterate = 1 also zeroes the
- * warm-start iterate and multipliers (acados_solver.reset(), gpmpc/mpc.py:147). */
+ * warm-start iterate and multipliers (acados_solver.reset(), gpmpc/mpc.py:62; and the fresh
+ * AcadosOcpSolver GPMPC.reset builds after new GPs, gpmpc/gpmpc.py:97-108). */
 gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, void* stream);
 
 /* Set the warm-start iterate (device arrays x [B][H+1][nx], u [B][H][nu]); multipliers zeroed. */
@@ -153,17 +158,24 @@ gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* para
 
 /* Kernel timing with HIP events recorded on the solve stream around the variance kernel
  * and the SQP kernel of every gpmpc_solve while enabled.  gpmpc_kernel_times synchronises
- * on the recorded events, returns the summed milliseconds and launch counts, and clears them. */
+ * on the recorded events, returns the summed milliseconds and launch counts, and clears them.
+ * gpmpc_kernel_time_list returns the per-launch milliseconds instead (host arrays of capacity
+ * `cap`; n_var / n_sqp receive the counts, at most cap are written) and clears them.
+ * Replaces the perf_counter around select_action, scripts/run_gp_mpc.py:55-57. */
 gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled);
 gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp);
+gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms, int32_t* n_var, double* sqp_ms,
+                                    int32_t* n_sqp);
 
 /* Diagnostic builds (-DGPMPC_TIMING) only: device buffer [max_batch][12] (uint64) receiving
  * per-phase shader-clock cycles of each instance's last solve; NULL disables. */
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
 
-/* Optional device buffer [max_batch][8] (int64) of running solver statistics, accumulated by the
+/* Optional device buffer [max_batch][10] (int64) of running solver statistics, accumulated by the
  * SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
- * of solves that ended with status s (0..4).  The caller zeroes it; NULL disables (default).
+ * of solves that ended with status s (0..4), [7] largest SQP iteration count of one solve,
+ * [8] largest QP iteration total of one solve, [9] reserved.  The caller zeroes it; NULL
+ * disables (default).
  * Replaces reading acados' per-solve "sqp_iter" / "qp_iter" / status stats in a host loop. */
 gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev);
 

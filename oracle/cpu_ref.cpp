@@ -13,7 +13,7 @@
 //   exact posterior variance + likelihood noise             gpmpc/gpmpc.py:441-445
 //   GP-augmented dynamics + RK4 + exact tangent map         gpmpc/gpmpc.py:166-221, gpmpc/mpc.py:65-88
 //   constraint tightening (covariance recursion)            gpmpc/gpmpc.py:425-498
-//   tightened box constraints (uh = -1e-8 / +1e-8)           gpmpc/gpmpc.py:275-332, gpmpc/mpc.py:210-255
+//   tightened box constraints (uh = -1e-8 / +1e-8)           gpmpc/gpmpc.py:275-332, gpmpc/mpc.py:125-170
 //   SQP-GN, full steps, acados status codes                 gpmpc/gpmpc.py:257-264, 334-368
 //   reference window                                        gpmpc/gpmpc.py:509-514
 // Conventions (variable layout d = [u_0, x_1, u_1, ..., x_T], the Mehrotra IPM, residual
@@ -37,8 +37,10 @@ enum { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };
 enum { kSuccess = 0, kNaN = 1, kMaxIter = 2, kQPFailure = 4 };
 
 struct GP {
-    int n = 0, d = 0;
-    std::vector<double> X, alpha, L;   // X [n][d], L lower Cholesky of K [n][n] (may be empty)
+    int n = 0, d = 0, nv = 0;
+    std::vector<double> X, alpha, L;   // X [n][d], L lower Cholesky of K(Xv, Xv) [nv][nv] (may be empty)
+    std::vector<double> Xv;            // variance rows [nv][d]; empty: Xv = X (exact GP).  FITC:
+                                       // mean over inducing rows X, variance over the training set
     double ell = 1, sf2 = 1, sn2 = 0;
     int in_idx[3] = {0, 0, 0}, var_idx[3] = {0, 0, 0};
 
@@ -63,14 +65,16 @@ struct GP {
     // sf2 - |L^-1 k|^2 + sn2  (exact posterior variance with the likelihood noise)
     double var(const double* z, std::vector<double>& v) const {
         const double c = -0.5 / (ell * ell);
-        v.resize(n);
+        const bool own = !Xv.empty();
+        const int m = own ? nv : n;
+        v.resize(m);
         double acc = 0.0;
-        for (int i = 0; i < n; ++i) {
-            const double* x = &X[(size_t)i * d];
+        for (int i = 0; i < m; ++i) {
+            const double* x = own ? &Xv[(size_t)i * d] : &X[(size_t)i * d];
             double q = 0.0;
             for (int k = 0; k < d; ++k) q += (x[k] - z[k]) * (x[k] - z[k]);
             double s = sf2 * std::exp(c * q);
-            const double* Li = &L[(size_t)i * n];
+            const double* Li = &L[(size_t)i * m];
             for (int j = 0; j < i; ++j) s -= Li[j] * v[j];
             v[i] = s / Li[i];
             acc += v[i] * v[i];
@@ -579,7 +583,17 @@ struct Instance {
         std::vector<double> d, pq, sl, su, l1, l2;
         int status = kMaxIter, it = 0;
         qp_total = 0;
-        for (it = 0; it <= P.max_iter; ++it) {
+        // stage-0 state rows (gpmpc/gpmpc.py:288,296,309-310; gpmpc/mpc.py:141,145,157-158): x_0 is
+        // pinned to obs, so they only decide feasibility; an obs outside the box by more than the
+        // inequality tolerance is an infeasible QP (acados status 4)
+        double v0 = 0.0;
+        for (int i = 0; i < nx; ++i) {
+            const double e = std::max(P.xlo[i] - P.uh - x0[i], x0[i] - P.xhi[i] - P.uh);
+            v0 = (e == e && v0 == v0) ? std::max(v0, e) : NAN;
+        }
+        const bool x0_ok = v0 <= P.tol;
+        if (!x0_ok) status = kQPFailure;
+        for (it = 0; x0_ok && it <= P.max_iter; ++it) {
             linearize(xs.data(), us.data());
             pack(xs.data(), us.data(), w.data());
             for (int i = 0; i < n; ++i) g[i] = hd[i] * (w[i] - yref[i]);
@@ -592,7 +606,10 @@ struct Instance {
             }
             for (int k = 0; k < H; ++k)
                 for (int i = 0; i < nx; ++i) re = std::max(re, std::fabs(F[k * nx + i] - xs[(k + 1) * nx + i]));
-            for (int i = 0; i < nx; ++i) ri = std::max(ri, std::fabs(x0[i] - xs[i]));
+            for (int i = 0; i < nx; ++i) {
+                ri = std::max(ri, std::fabs(x0[i] - xs[i]));
+                ri = std::max(ri, std::max(P.xlo[i] - P.uh - xs[i], xs[i] - P.xhi[i] - P.uh));
+            }
             if (trace) std::fprintf(stderr, "  sqp %d: stat %.3e eq %.3e ineq %.3e comp %.3e (qp iters so far %d)\n", it, rs, re, ri, rc, qp_total);
             if (!(rs == rs && re == re && ri == ri && rc == rc)) { status = kNaN; break; }
             if (rs <= P.tol && re <= P.tol && ri <= P.tol && rc <= P.tol) { status = kSuccess; break; }
@@ -622,8 +639,15 @@ struct Instance {
             for (double v : us) fin = fin && std::isfinite(v);
             if (!fin) { status = kNaN; break; }
         }
-        x = xs;
-        u = us;
+        const bool good = status == kSuccess || status == kMaxIter;
+        if (good) {
+            x = xs;
+            u = us;
+        } else {   // a failed solve keeps the previous iterate and restarts the multipliers
+            std::fill(pi.begin(), pi.end(), 0.0);
+            std::fill(ll.begin(), ll.end(), 0.0);
+            std::fill(lu.begin(), lu.end(), 0.0);
+        }
         sqp_iter = it;
         for (int a = 0; a < nu; ++a) u0[a] = u[a];
         return status;
@@ -677,6 +701,8 @@ int cpuref_set_gp(void* h, int g, int n, int d, const double* X, const double* a
     GP& G = P.gp[g];
     G.n = n;
     G.d = d;
+    G.nv = 0;
+    G.Xv.clear();
     G.X.assign(X, X + (size_t)n * d);
     G.alpha.assign(alpha, alpha + n);
     if (L) G.L.assign(L, L + (size_t)n * n); else G.L.clear();
@@ -684,6 +710,20 @@ int cpuref_set_gp(void* h, int g, int n, int d, const double* X, const double* a
     G.sf2 = sf2;
     G.sn2 = sn2;
     for (int k = 0; k < d; ++k) { G.in_idx[k] = in_idx[k]; G.var_idx[k] = var_idx[k]; }
+    return 0;
+}
+
+// FITC: the variance of GP g runs over its own rows Xv [nv][d] (the training set) with L the
+// Cholesky factor of K(Xv, Xv) [nv][nv], while cpuref_set_gp's X / alpha are the inducing rows and
+// weights of the mean (gpmpc/gpmpc.py:175-187 mean, :441-445 exact variance).
+int cpuref_set_gp_var(void* h, int g, int nv, const double* Xv, const double* L) {
+    Problem& P = static_cast<Handle*>(h)->P;
+    if (g < 0 || g >= P.ngp || nv < 1 || !Xv || !L) return -1;
+    GP& G = P.gp[g];
+    if (G.d < 1) return -1;
+    G.nv = nv;
+    G.Xv.assign(Xv, Xv + (size_t)nv * G.d);
+    G.L.assign(L, L + (size_t)nv * nv);
     return 0;
 }
 
@@ -733,7 +773,7 @@ int cpuref_step(void* h, int B, const double* x0, const int* tstep, double* xs, 
             status[b] = I.step(x0 + (size_t)b * nx, tstep[b], has_prev[b] != 0, u0 + (size_t)b * nu, si, qi);
             sqp_iter[b] = si;
             qp_iter[b] = qi;
-            has_prev[b] = 1;
+            has_prev[b] = (status[b] == kSuccess || status[b] == kMaxIter) ? 1 : 0;
             std::copy(I.x.begin(), I.x.end(), xs + (size_t)b * (H + 1) * nx);
             std::copy(I.u.begin(), I.u.end(), us + (size_t)b * H * nu);
             std::copy(I.pi.begin(), I.pi.end(), pi + (size_t)b * H * nx);

@@ -18,6 +18,7 @@ _SIGS = {
     "cpuref_destroy": (None, [_P]),
     "cpuref_set_options": (None, [_P, _I, _D, _I, _D]),
     "cpuref_set_gp": (_I, [_P, _I, _I, _I, _P, _P, _P, _D, _D, _D, _P, _P]),
+    "cpuref_set_gp_var": (_I, [_P, _I, _I, _P, _P]),
     "cpuref_use_gp": (None, [_P, _I]),
     "cpuref_set_tightening": (None, [_P, _I, _D, _P, _P, _P, _P, _I]),
     "cpuref_set_reference": (None, [_P, _P, _I]),
@@ -47,7 +48,9 @@ class CpuRef:
     """B instances of the control step on the host (GPMPC.select_action semantics, batched)."""
 
     def __init__(self, spec, H: int, B: int, gps=None, lqr_mats=None, prob: float = 0.95, uh: float = -1e-8,
-                 tol: float = 1e-6, qp_tol: float = 1e-8, qp_max_iter: int = 50, max_iter: int = 25):
+                 tol: float = 1e-6, qp_tol: float = 1e-8, qp_max_iter: int = 50, max_iter: int = 25, fitc=None):
+        """``fitc[g] = (S (M, d), w (M,))``: GP g's mean over the inducing rows S with weights w
+        (`gpmpc/gpmpc.py:175-187,377-400`); its variance stays the exact GP's (``gps[g]``)."""
         from oracle import gpmpc_oracle as O
 
         self.lib = load()
@@ -71,8 +74,15 @@ class CpuRef:
                 ii = _c(spec.gp_inputs[g], np.int32)
                 vi = _c(spec.var_inputs[g], np.int32)
                 self._keep += [X, a, L, ii, vi]
-                rc = self.lib.cpuref_set_gp(self.h, g, X.shape[0], X.shape[1], X.ctypes.data, a.ctypes.data,
-                                            L.ctypes.data, gp.ell, gp.sf2, gp.sn2, ii.ctypes.data, vi.ctypes.data)
+                if fitc is not None and fitc[g] is not None:
+                    S, w = _c(fitc[g][0]), _c(fitc[g][1])
+                    self._keep += [S, w]
+                    rc = self.lib.cpuref_set_gp(self.h, g, S.shape[0], S.shape[1], S.ctypes.data, w.ctypes.data,
+                                                None, gp.ell, gp.sf2, gp.sn2, ii.ctypes.data, vi.ctypes.data)
+                    rc = rc or self.lib.cpuref_set_gp_var(self.h, g, X.shape[0], X.ctypes.data, L.ctypes.data)
+                else:
+                    rc = self.lib.cpuref_set_gp(self.h, g, X.shape[0], X.shape[1], X.ctypes.data, a.ctypes.data,
+                                                L.ctypes.data, gp.ell, gp.sf2, gp.sn2, ii.ctypes.data, vi.ctypes.data)
                 if rc != 0:
                     raise RuntimeError(f"cpuref_set_gp({g}) failed")
             self.lib.cpuref_use_gp(self.h, 1)

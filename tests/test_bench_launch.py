@@ -1,0 +1,40 @@
+"""bench.py's multi-rank path on the CPU: ``--gpus 2`` without torchrun launches two ranks
+itself (gpmpc/launch.py), the ranks own contiguous instance shards, and the reported time is the
+max over ranks (the driver runs ``bench.py --gpus N`` on one node)."""
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _run(args):
+    env = dict(os.environ, GPMPC_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=env,
+                       timeout=240, cwd=str(ROOT))
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout   # rank 0 prints exactly one line
+    return json.loads(lines[0])
+
+
+def test_self_launch_two_ranks_shards_and_max_timing():
+    B, steps = 8, 6
+    out = _run(["--gpus", "2", "--dry-run", "--batch", str(B), "--steps", str(steps), "--warmup", "1"])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 2 * B
+    shards = out["shards"]
+    assert [s[:2] for s in shards] == [[0, B], [B, 2 * B]]          # contiguous, disjoint, covering
+    # rank r sleeps (1 + r) ms per step: the job time is the slowest rank's, not rank 0's
+    slowest = max(s[2] for s in shards)
+    assert slowest >= steps * 2e-3
+    assert out["ms_per_step"] * 1e-3 * steps >= slowest - 1e-9
+    assert abs(out["value"] - 2 * B * steps / (out["ms_per_step"] * 1e-3 * steps)) <= 1e-6 * out["value"]
+
+
+def test_single_rank_needs_no_launcher():
+    out = _run(["--gpus", "1", "--dry-run", "--batch", "4", "--steps", "2", "--warmup", "0"])
+    assert out["n_gpus"] == 1 and out["shards"] == [[0, 4, out["shards"][0][2]]]

@@ -112,3 +112,62 @@ def test_two_rank_gp_fit_allreduce_matches_single_process():
     ref = GaussianProcess(torch.tensor(X), torch.tensor(y))
     fit_gp(ref, n_train=40, lr=0.05)
     np.testing.assert_allclose(res[0][2:], [ref.lengthscale, ref.outputscale, ref.noise], rtol=1e-8)
+
+
+def _gather_worker(rank, world, port, out):
+    sys.path[:0] = [str(ROOT / "gp-mpc_amd"), str(ROOT)]
+    import torch
+    import torch.distributed as dist
+
+    from gpmpc import distributed as D
+    from gpmpc.gp import GaussianProcess
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # each rank sampled its own transitions (different counts too): learning.learn gathers them
+    rng = np.random.default_rng([5, rank])
+    n = 12 + 3 * rank
+    inputs = rng.uniform(-1, 1, size=(n, 3))
+    targets = np.sin(2 * inputs[:, :1]) + 0.01 * rng.standard_normal((n, 1))
+    x_train, y_train = D.gather_rows(inputs), D.gather_rows(targets)
+    D.assert_replicated(x_train, y_train)          # identical replicas: no error
+    try:
+        D.assert_replicated(inputs)                # rank-local data: must be refused
+        refused = False
+    except RuntimeError:
+        refused = True
+    gp = GaussianProcess(torch.tensor(x_train), torch.tensor(y_train[:, 0]))
+    it = D.fit_gp_allreduce(gp, n_train=30, lr=0.05)
+    out.put((rank, x_train.tolist(), y_train.tolist(), refused, it, gp.lengthscale, gp.outputscale, gp.noise))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_learning_epoch_gathers_transitions_before_the_fit():
+    """per-epoch all-gather of the newly sampled transitions, so both ranks fit
+    identical GPs on identical x_train (gpmpc/learning.py learn; `scripts/run_gp_mpc.py:115-120`)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    r0, r1 = res
+    assert r0[1] == r1[1] and r0[2] == r1[2]                 # identical x_train / y_train
+    assert len(r0[1]) == 12 + 15                             # rank 0's 12 rows then rank 1's 15
+    rng0 = np.random.default_rng([5, 0])
+    np.testing.assert_array_equal(np.array(r0[1][:12]), rng0.uniform(-1, 1, size=(12, 3)))
+    assert r0[3] and r1[3]                                   # rank-local data is refused
+    assert r0[4:] == r1[4:]                                  # identical fitted hyperparameters
+    sys.path[:0] = [str(ROOT / "gp-mpc_amd")]
+    import torch
+
+    from gpmpc.gp import GaussianProcess, fit_gp
+
+    ref = GaussianProcess(torch.tensor(np.array(r0[1])), torch.tensor(np.array(r0[2])[:, 0]))
+    fit_gp(ref, n_train=30, lr=0.05)
+    np.testing.assert_allclose(r0[5:], [ref.lengthscale, ref.outputscale, ref.noise], rtol=1e-8)

@@ -1,4 +1,4 @@
-"""End-to-end learning loop on the MI355X (`scripts/run_gp_mpc.py:89-137`): prior MPC episodes,
+"""End-to-end learning loop on the MI355X (`scripts/run_gp_mpc.py:86-137`): prior MPC episodes,
 preprocess_data, GP fit on the GPU, GP-MPC episodes; batched synthetic plant."""
 
 import numpy as np

@@ -1,0 +1,149 @@
+"""Semantics of the drop-in surface on the MI355X (through the C ABI):
+
+* stage-0 state rows: an obs outside the box is status 4 (`gpmpc/gpmpc.py:288,296,309-310`),
+  on the bound (within the tolerance) it solves; a failed instance keeps its previous iterate,
+  returns its first input and recovers on the next step (no NaN poisoning); the drop-in
+  ``GPMPC.select_action`` asserts on it like the reference (`gpmpc/gpmpc.py:365`);
+* ``GPMPC.reset`` after new GPs starts from a fresh iterate, as the reference's new
+  ``AcadosOcpSolver`` (`gpmpc/gpmpc.py:97-108`); with unchanged GPs it keeps the warm start;
+* ``MPC(q_mpc, r_mpc)`` solves the OCP with those weights (`gpmpc/mpc.py:42-45`).
+"""
+
+import numpy as np
+import pytest
+
+from helpers import O, initial_states, lqr, oracle_gps, oracle_step, problem, product_gps
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def test_infeasible_and_nan_obs_fail_without_poisoning():
+    torch = _torch()
+    from oracle import cpu_ref
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem("quad2d", 60)
+    H, B = 12, 4
+    mats = lqr(spec)
+    gs = BatchSolver(spec, H, B)
+    gs.set_gps(product_gps(data, hyp))
+    gs.set_tightening(True, 0.95, *mats)
+    gs.reset(reset_iterate=True)
+    have_ref = cpu_ref.LIB_PATH.exists()
+    ref = cpu_ref.CpuRef(spec, H, B, gps=oracle_gps(data, hyp), lqr_mats=mats) if have_ref else None
+    traj = spec.reference_trajectory()
+    x0, ph = initial_states(spec, traj, B)
+
+    def solve(x, k):
+        u = gs.solve(torch.tensor(x, device="cuda"), torch.tensor(ph + k, dtype=torch.int32, device="cuda"))
+        if ref is not None:
+            ref.step(x, ph + k)
+        return u.cpu().numpy(), gs.status.cpu().numpy()
+
+    u, st = solve(x0, 0)
+    assert (st == 0).all()
+    xp, up, _ = (t.cpu().numpy() for t in gs.solution())
+    bad = x0.copy()
+    bad[1, 2] = spec.x_hi[2] + 0.1                    # z above the box: infeasible stage-0 row
+    bad[2, 0] = np.nan                                # NaN observation
+    bad[3, 4] = spec.x_hi[4] - 1e-8                   # theta exactly on its stage-0 bound: feasible
+    bad[3, 5] = 0.0                                   # (at rest, so the next stages can stay inside)
+    u, st = solve(bad, 1)
+    assert st[0] == 0 and st[1] == 4 and st[2] == 4 and st[3] in (0, 2), st
+    if ref is not None:
+        np.testing.assert_array_equal(st, ref.status)
+    x1, u1, _ = (t.cpu().numpy() for t in gs.solution())
+    np.testing.assert_array_equal(x1[1:3], xp[1:3])     # failed instances keep the previous iterate
+    np.testing.assert_array_equal(u[1:3], up[1:3, 0])   # ... and return its first input
+    assert np.isfinite(x1).all() and np.isfinite(u).all()
+    u, st = solve(x0, 2)
+    assert (st == 0).all() and np.isfinite(u).all(), st
+    if ref is not None:
+        np.testing.assert_array_equal(st, ref.status)
+        x2 = gs.solution()[0].cpu().numpy()
+        err = np.abs(x2 - ref.x).max() / (1 + np.abs(ref.x).max())
+        assert err <= 1e-5, err
+
+
+def test_gpmpc_select_action_asserts_on_infeasible_obs():
+    _torch()
+    from gpmpc.gpmpc import GPMPC
+
+    spec, data, hyp = problem("quad2d", 40)
+    ctrl = GPMPC("quad2d", horizon=10, prob=0.95)
+    ctrl.set_gaussian_processes(product_gps(data, hyp))
+    ctrl.reset()
+    x = initial_states(spec, spec.reference_trajectory(), 1)[0][0]
+    ctrl.select_action(x)
+    bad = x.copy()
+    bad[0] = spec.x_hi[0] + 1.0
+    with pytest.raises(AssertionError, match="status 4"):
+        ctrl.select_action(bad)
+    ctrl.select_action(x)   # the controller is usable again
+
+
+def test_gpmpc_reset_after_new_gps_restarts_the_iterate():
+    torch = _torch()
+    from gpmpc.gpmpc import GPMPC
+
+    spec, data, hyp = problem("quad2d", 50)
+    x = initial_states(spec, spec.reference_trajectory(), 1)[0][0]
+    gps = product_gps(data, hyp)
+
+    def run(ctrl, steps):
+        out = []
+        for _ in range(steps):
+            out.append(ctrl.select_action(x))
+        return out, int(ctrl.solver.sqp_iter[0])
+
+    fresh = GPMPC("quad2d", horizon=10, prob=0.95)
+    fresh.set_gaussian_processes(gps)
+    fresh.reset()
+    (u_fresh,), it_fresh = run(fresh, 1)
+
+    ctrl = GPMPC("quad2d", horizon=10, prob=0.95)
+    ctrl.set_gaussian_processes(gps)
+    ctrl.reset()
+    run(ctrl, 3)                                     # the iterate now holds a converged solution
+    ctrl.set_gaussian_processes(gps)                 # "retrained": the reference rebuilds its solver
+    ctrl.reset()
+    (u_new,), it_new = run(ctrl, 1)
+    np.testing.assert_array_equal(u_new, u_fresh)    # bitwise: same inputs from a zero iterate
+    assert it_new == it_fresh
+    ctrl.reset()                                     # same GPs: acados keeps its memory
+    (u_warm,), it_warm = run(ctrl, 1)
+    assert it_warm < it_fresh                        # warm-started from the last solution
+
+
+def test_mpc_q_r_weights_change_the_solution():
+    _torch()
+    from gpmpc.mpc import MPC
+
+    spec, _, _ = problem("cartpole", 10)
+    H = 10
+    traj = spec.reference_trajectory()
+    x = initial_states(spec, traj, 1)[0][0]
+    q2 = np.array([5.0, 0.5, 2.0, 0.2])
+    r2 = np.array([0.02])
+    u = {}
+    for name, (q, r) in {"default": (spec.q_diag, spec.r_diag), "custom": (q2, r2)}.items():
+        ctrl = MPC("cartpole", q_mpc=list(q), r_mpc=list(r), horizon=H)
+        ctrl.reset()
+        u[name] = ctrl.select_action(x)
+        sd = spec.to_dict()
+        sd["q_diag"], sd["r_diag"] = np.asarray(q), np.asarray(r)
+        orc = O.SQPSolver(sd, O.Dynamics(sd, None), H, O.SQPOptions(qp_tol=1e-10, qp_max_iter=100))
+        sp = spec.copy()
+        sp.q_diag, sp.r_diag = np.asarray(q), np.asarray(r)
+        st, _, _ = oracle_step(sp, orc, None, x, 0, H, traj, None, tighten=False, uh=1e-8)
+        assert st == 0
+        assert np.abs(u[name] - orc.u[0]).max() <= 1e-4 * (1 + np.abs(orc.u).max()), (name, u[name], orc.u[0])
+    assert np.abs(u["default"] - u["custom"]).max() > 1e-3

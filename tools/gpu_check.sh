@@ -8,7 +8,7 @@ OUT=${1:?outdir}
 shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
-timeout -k 10 420 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1
 timeout -k 10 180 python3 -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 timeout -k 10 300 python3 -u bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
