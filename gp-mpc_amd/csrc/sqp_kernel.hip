@@ -57,6 +57,15 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// Lanes in the banks (quads of a 16-lane row) selected by BANK receive v's DPP-moved value, the
+// others keep `old` (the update_dpp old-value semantics).
+template <int CTRL, int BANK>
+__device__ __forceinline__ double dpp_merge(double old, double v) {
+    const long long o = __double_as_longlong(old), b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, 0xf, BANK, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, 0xf, BANK, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 __device__ __forceinline__ double xor16_d(double v) {   // value of lane l ^ 16
     const long long b = __double_as_longlong(v);
     const auto lo = __builtin_amdgcn_permlane16_swap((int)b, (int)b, false, false);
@@ -814,6 +823,7 @@ struct SqpKernel {
     //   Schur onto the state block       Ru by readlane, row/column slices by lane shuffles
     __device__ static int pidx(int i, int j) { return i * NX - (i * (i - 1)) / 2 + (j - i); }  // i <= j < NX
 
+    template <bool kSchurN = false>
     __device__ static bool mfma_backward(const Lds& L, int H, int lane) {
         const int lr = lane >> 4, lc = lane & 15;
         const bool colok = (lc < NX) || (lc == NB);
@@ -932,18 +942,20 @@ struct SqpKernel {
             else mu = __shfl(m[SE], (((lr + SG) & 3) << 4) | lc);
             // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff);
             // rows a >= NU meet a zero A operand and need no mask
-            double kb, Ri[NU][NU];
+            double kb, Ri[NU][NU], num = 0.0, id = 0.0;
             if constexpr (NU == 1) {
                 ok = ok && (Ru[0][0] > 0.0);
-                Ri[0][0] = fast_rcp(Ru[0][0]);
-                kb = -Ri[0][0] * mu;
+                id = fast_rcp(Ru[0][0]);
+                Ri[0][0] = id;
+                num = mu;
+                kb = -id * mu;
             } else {
                 const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
                 ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
                 // lane a=0: mu = M'[NX], mo = M'[NX+1]; lane a=1: mu = M'[NX+1], mo = M'[NX]
                 const double mo = xor16_d(mu);
-                const double num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
-                const double id = fast_rcp(det);
+                num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
+                id = fast_rcp(det);
                 kb = num * -id;
                 Ri[0][0] = Ru[1][1] * id;
                 Ri[1][1] = Ru[0][0] * id;
@@ -955,8 +967,16 @@ struct SqpKernel {
                 *srui = rv;
                 srui -= srui_st;
             }
-            // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M')
-            const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);
+            // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M').  kSchurN: the numerator product
+            // N = M'_xu adj(Ru) M'_u runs on the matrix core while det / rcp run on the VALU, and
+            // P'_k = M' - N / det is one fma per register (rows 8..15 keep M', finite and unread).
+            f64x4 pk;
+            if constexpr (kSchurN) {
+                const f64x4 nk = mfma64(lr < NU ? mu : 0.0, num, f64x4{0.0, 0.0, 0.0, 0.0});
+                pk = f64x4{fma(-id, nk[0], m[0]), fma(-id, nk[1], m[1]), m[2], m[3]};
+            } else {
+                pk = mfma64(lr < NU ? mu : 0.0, kb, m);
+            }
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 // branch-free store: entries that are not stored go to a dummy slot
@@ -1042,36 +1062,99 @@ struct SqpKernel {
         }
     }
 
-    // Forward sweep on MFMA: X_{k+1} = A'_k [dx_k; 1] with X held in column 0 of a C tile,
-    // which is also the B operand of the next stage's product.
-    __device__ static void mfma_forward(const Lds& L, int H, int lane) {
-        const int lr = lane >> 4, lc = lane & 15;
-        double xb[2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) xb[s2] = (lc == 0 && lr + 4 * s2 == NX) ? 1.0 : 0.0;
-        if (lane < NX) L.dxv[lane] = 0.0;
-        auto load_stage = [&](int k, double (&a)[2]) {
-            const double* A = L.Acl + (size_t)k * NX * PS;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int col = lr + 4 * s2;
-                const bool ok = lc < NX && col < PS;
-                const double v = A[ok ? lc * PS + col : 0];
-                a[s2] = ok ? v : 0.0;
+    // ------------------------------------------------------------------ sweeps on v_mfma_f64_4x4x4_4b
+    // An affine recurrence y_{k+1} = M_k y_k over the homogeneous 8-vector y = [v (NX); 1; 0] (4 <= NX <= 6)
+    // as ONE 4-block MFMA per stage.  Lane l = 16r + 4b + c: the instruction's block b takes A_b[m][k]
+    // from lane (k, b, m) and B_b[k][n] from lane (k, b, n) and writes D_b[m][n] to lane (m, b, n)
+    // (tools/probe_mfma4x4.hip), so D lands in the B layout of the next stage.  Blocks:
+    //   b = 0: M_ll y_lo   b = 1: M_lh y_hi   b = 2: M_hh y_hi   b = 3: M_hl y_lo
+    // (lo/hi = rows or columns 0..3 / 4..7), every column n carrying the same vector.  Then
+    //   S = D + (D of the next quad)          quad 0: y'_lo, quad 2: y'_hi   (DPP row_ror:12 + one add)
+    //   B' = S, quads 1 and 3 <- next quad     quads (lo, hi, hi, lo)         (one bank-masked DPP move)
+    // so a stage is MFMA -> DPP -> add -> DPP on the chain instead of a 6-term dot product behind
+    // v_readlane broadcasts.  The stage operands M_k are loaded one stage ahead (one LDS read per lane).
+    struct Mfma4Lane {
+        int r, b, c, row, col;
+    };
+    __device__ static Mfma4Lane mfma4_lane(int lane) {
+        Mfma4Lane q;
+        q.r = lane >> 4;
+        q.b = (lane >> 2) & 3;
+        q.c = lane & 3;
+        q.row = ((q.b >> 1) ? 4 : 0) + q.c;                    // row of M_k this lane supplies (A_b[m = c])
+        q.col = ((q.b == 1 || q.b == 2) ? 4 : 0) + q.r;        // column (A_b[k = r])
+        return q;
+    }
+    // y (B layout) of the homogeneous vector [v; 1; 0] with v[i] = vget(i)
+    template <class F>
+    __device__ static double mfma4_vec(const Mfma4Lane& q, F&& vget) {
+        const int idx = ((q.b == 1 || q.b == 2) ? 4 : 0) + q.r;
+        return idx < NX ? vget(idx) : (idx == NX ? 1.0 : 0.0);
+    }
+    // One stage: D = M_k y; returns y_{k+1} in the B layout and the stage output in `s`
+    // (lanes (r, 0, c): v'[r], lanes (r, 2, c): v'[4 + r]).
+    __device__ static double mfma4_stage(double a, double y, double& s) {
+        const double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a, y, 0.0, 0, 0, 0);
+        s = d + dpp_d<0x12C>(d);                  // row_ror:12: lane i <- lane (i + 4) mod 16
+        return dpp_merge<0x12C, 0xA>(s, s);       // quads 1, 3 <- quads 2, 0
+    }
+
+    // Forward sweep: dx_0 = 0, dx_{k+1} = A'_k [dx_k; 1]  (M_k = [A'_k; e_NX]).  Masked lanes read the
+    // LDS zero slot (stride 0) and the homogeneous corner the one slot, so the stage operand is one
+    // unconditional load issued a stage ahead.
+    template <int VAR = 0>
+    __device__ static void mfma4_forward(const Lds& L, int H, int lane) {
+        static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
+        if constexpr (VAR == 0) {
+            const Mfma4Lane q = mfma4_lane(lane);
+            const bool ld = q.row < NX && q.col <= NX;
+            const double* src = ld ? L.Acl + q.row * PS + q.col : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0);
+            const int st = ld ? NX * PS : 0;
+            const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+            const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+            double* out = stlo ? L.dxv + NX + q.r : (sthi ? L.dxv + NX + 4 + q.r : L.dummy + lane);
+            const int ost = (stlo || sthi) ? NX : 0;
+            if (lane < NX) L.dxv[lane] = 0.0;
+            double y = mfma4_vec(q, [](int) { return 0.0; });
+            double an = *src;
+            for (int k = 0; k < H; ++k) {
+                const double a = an;
+                src += (k + 1 < H) ? st : 0;
+                an = *src;
+                double s;
+                y = mfma4_stage(a, y, s);
+                *out = s;
+                out += ost;
             }
-        };
-        double an[2];
-        load_stage(0, an);
-        for (int k = 0; k < H; ++k) {
-            double a[2] = {an[0], an[1]};
-            if (k + 1 < H) load_stage(k + 1, an);
-            f64x4 acc = mfma64(a[0], xb[0], f64x4{0.0, 0.0, 0.0, 0.0});
-            acc = mfma64(a[1], xb[1], acc);
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int row = lr + 4 * s2;
-                xb[s2] = (lc == 0) ? (row < NX ? acc[s2] : (row == NX ? 1.0 : 0.0)) : 0.0;
-                if (lc == 0 && row < NX) L.dxv[(size_t)(k + 1) * NX + row] = acc[s2];
+        } else {
+            // two chained MFMAs per stage: block b computes row block (b & 1) of M_k y over the two
+            // K blocks, so D lands as (y'_lo, y'_hi, y'_lo, y'_hi); the next B operands are y_lo and
+            // y_hi in every block (two bank-masked DPP moves, independent of each other)
+            const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
+            const int row = ((b & 1) ? 4 : 0) + c;
+            const bool l1 = row < NX && r <= NX, l2 = row < NX && 4 + r <= NX;
+            const double* s1 = l1 ? L.Acl + row * PS + r : L.zero + ((row == NX && r == NX) ? 7 : 0);
+            const double* s2 = l2 ? L.Acl + row * PS + 4 + r : L.zero + ((row == NX && 4 + r == NX) ? 7 : 0);
+            const int st1 = l1 ? NX * PS : 0, st2 = l2 ? NX * PS : 0;
+            const bool stlo = b == 0 && c == 0 && r < NX;
+            const bool sthi = b == 1 && c == 0 && 4 + r < NX;
+            double* out = stlo ? L.dxv + NX + r : (sthi ? L.dxv + NX + 4 + r : L.dummy + lane);
+            const int ost = (stlo || sthi) ? NX : 0;
+            if (lane < NX) L.dxv[lane] = 0.0;
+            double ylo = 0.0, yhi = (4 + r == NX) ? 1.0 : 0.0;
+            double a1n = *s1, a2n = *s2;
+            for (int k = 0; k < H; ++k) {
+                const double a1 = a1n, a2 = a2n;
+                s1 += (k + 1 < H) ? st1 : 0;
+                s2 += (k + 1 < H) ? st2 : 0;
+                a1n = *s1;
+                a2n = *s2;
+                double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, ylo, 0.0, 0, 0, 0);
+                d = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, yhi, d, 0, 0, 0);
+                *out = d;
+                out += ost;
+                ylo = dpp_merge<0x124, 0xA>(d, d);   // quads 1, 3 <- quads 0, 2 (row_ror:4)
+                yhi = dpp_merge<0x12C, 0x5>(d, d);   // quads 0, 2 <- quads 1, 3 (row_ror:12)
             }
         }
     }
@@ -1118,6 +1201,7 @@ struct SqpKernel {
     // with [q; r] = gq.  Only the p recurrence is sequential (6-term VALU dot products with
     // readlane broadcast); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
+    template <bool kMfma4 = false>
     __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
@@ -1160,6 +1244,33 @@ struct SqpKernel {
             if (has1) VT[e1] = a1;
         }
         WSYNC();
+        if constexpr (kMfma4) {
+            // p_k = vt_k + A'_k^T p_{k+1} as the homogeneous recurrence [p_k; 1] = M_k [p_{k+1}; 1],
+            // M_k = [[A'_k[:, :NX]^T, vt_k], [0, 1]] (mfma4_stage), stages H-1 .. 0
+            const Mfma4Lane q = mfma4_lane(lane);
+            const bool lda = q.row < NX && q.col < NX, ldv = q.row < NX && q.col == NX;
+            const double* src = lda ? L.Acl + (size_t)(H - 1) * NX * PS + q.col * PS + q.row
+                                    : (ldv ? VT + (size_t)(H - 1) * NX + q.row
+                                           : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0));
+            const int st = lda ? NX * PS : (ldv ? NX : 0);
+            if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
+            double y = mfma4_vec(q, [&](int i) { return L.gq[H * NB + i]; });
+            const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+            const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+            double* out = stlo ? L.P + (size_t)(H - 1) * PP + PO + q.r
+                               : (sthi ? L.P + (size_t)(H - 1) * PP + PO + 4 + q.r : L.dummy + lane);
+            const int ost = (stlo || sthi) ? PP : 0;
+            double an = *src;
+            for (int k = H - 1; k >= 0; --k) {
+                const double a = an;
+                src -= (k >= 1) ? st : 0;
+                an = *src;
+                double sv;
+                y = mfma4_stage(a, y, sv);
+                *out = sv;
+                out -= ost;
+            }
+        } else {
         const int col = lane < NX ? lane : 0;
         double p = L.gq[H * NB + col];
         if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
@@ -1192,6 +1303,7 @@ struct SqpKernel {
             step(k - 1, c1);
         }
         if (k == 0) step(0, c0);
+        }
         WSYNC();
         for (int e = lane; e < H * NU; e += 64) {
             const int k = e / NU, a = e - k * NU;
@@ -1368,7 +1480,7 @@ struct SqpKernel {
         const int b = blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve(smem, H);
-        if (lane < 8) L.zero[lane] = 0.0;   // read by the masked stage-operand streams
+        if (lane < 8) L.zero[lane] = (lane == 7) ? 1.0 : 0.0;   // read by the masked stage-operand streams (7: one)
         const bool on = lane <= H;
         const bool act_x = on && lane >= 1;
         const bool act_u = lane < H;
@@ -1666,7 +1778,11 @@ struct SqpKernel {
                         acl_phase<true>(L, H, lane);
                         WSYNC();
                         TPHASE(6);
+#ifdef GPMPC_SWEEP_VALU
                         valu_forward(L, H, lane);
+#else
+                        mfma4_forward(L, H, lane);
+#endif
                         WSYNC();
                         TPHASE(9);
                         recover_q<NV>(L, H, kq, vb, dd, dp);
@@ -1722,12 +1838,20 @@ struct SqpKernel {
                     WSYNC();
                     TPHASE(5);
                     if constexpr (kMfma) {
-                        valu_vector_backward(L, H, lane);
+#ifdef GPMPC_SWEEP_VALU
+                        valu_vector_backward<false>(L, H, lane);
+#else
+                        valu_vector_backward<true>(L, H, lane);
+#endif
                         TPHASE(8);
                         acl_phase<false>(L, H, lane);
                         WSYNC();
                         TPHASE(6);
+#ifdef GPMPC_SWEEP_VALU
                         valu_forward(L, H, lane);
+#else
+                        mfma4_forward(L, H, lane);
+#endif
                         WSYNC();
                         TPHASE(9);
                         recover_q<NV>(L, H, kq, vb, dd, dp);

@@ -67,12 +67,15 @@ def main():
         u0 = s.solve(obs, ts)
         s.plant_step(obs, u0, ts, out=obs)
     tot = np.zeros(len(PHASES))
+    crit = np.zeros(len(PHASES))   # the slowest instance of each step (it sets the kernel time)
     s.set_profiling(True)
     s.kernel_times()
     for _ in range(args.steps):
         u0 = s.solve(obs, ts)
         torch.cuda.synchronize()
-        tot += tbuf.cpu().numpy().mean(0)
+        tb = tbuf.cpu().numpy().astype(np.float64)
+        tot += tb.mean(0)
+        crit += tb[np.argmax(tb[:, :-1].sum(1))]
         s.plant_step(obs, u0, ts, out=obs)
     kt = s.kernel_times()
     cyc = tot / args.steps
@@ -82,9 +85,13 @@ def main():
     print(f"{spec.name} B={B} H={H} N={N}: sqp kernel {ms:.3f} ms/launch, sqp_iter {s.sqp_iter.float().mean():.2f}, "
           f"qp_iter {s.qp_iter.float().mean():.2f}")
     print(f"cycles per instance (mean) {cyc.sum():.0f} -> {cyc.sum() / (ms * 1e-3) / 1e9:.2f} G cycles/s effective")
-    for name, c in zip(PHASES, cyc):
-        print(f"  {name:12s} {c:12.0f} cycles  {100 * c / cyc.sum():5.1f} %")
-    print(f"  {PHASES[-1]} {sub:.0f} cycles  {100 * sub / cyc.sum():5.1f} %")
+    crit /= args.steps
+    csub, crit = crit[-1], crit[:-1]
+    print(f"{'phase':26s} {'mean instance':>22s} {'slowest instance per step':>30s}")
+    for name, c, k in zip(PHASES, cyc, crit):
+        print(f"  {name:24s} {c:10.0f} cyc {100 * c / cyc.sum():5.1f} %   {k:10.0f} cyc {100 * k / crit.sum():5.1f} %")
+    print(f"  {PHASES[-1]:24s} {sub:10.0f} cyc {100 * sub / cyc.sum():5.1f} %   {csub:10.0f} cyc {100 * csub / crit.sum():5.1f} %")
+    print(f"  {'total':24s} {cyc.sum():10.0f} cyc           {crit.sum():10.0f} cyc")
 
 
 if __name__ == "__main__":

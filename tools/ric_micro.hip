@@ -18,7 +18,7 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     const auto L = KQ::carve(smem, H);
     const int lane = threadIdx.x;
     constexpr int NX = KQ::NX, NB = KQ::NB, GS = KQ::GS, PS = KQ::PS;
-    if (lane < 8) L.zero[lane] = 0.0;
+    if (lane < 8) L.zero[lane] = (lane == 7) ? 1.0 : 0.0;
     // synthetic, well-conditioned stage data: G' = [I + 0.01 R | 0.1 R | 0.01], hq >= 1
     for (int e = lane; e < H * NX * GS; e += 64) {
         const int j = e % GS, i = (e / GS) % NX;
@@ -37,10 +37,13 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int r = 0; r < reps; ++r) {
         if constexpr (V == 0) KQ::mfma_backward(L, H, lane);
+        if constexpr (V == 7) KQ::mfma_backward<true>(L, H, lane);
+        if constexpr (V == 8) KQ::mfma4_forward<1>(L, H, lane);
         if constexpr (V == 1) KQ::valu_vector_backward(L, H, lane);
         if constexpr (V == 2) KQ::template acl_phase<true>(L, H, lane);
-        if constexpr (V == 3) KQ::mfma_forward(L, H, lane);
+        if constexpr (V == 3) KQ::mfma4_forward(L, H, lane);
         if constexpr (V == 4) KQ::valu_forward(L, H, lane);
+        if constexpr (V == 6) KQ::valu_vector_backward<true>(L, H, lane);
         if constexpr (V == 5) { double v = (double)r; for (int q = 0; q < H; ++q) v = wave_sum(v) * 1e-3; L.dummy[lane] = v; }
         WSYNC();
     }
@@ -48,6 +51,92 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     if (lane == 0) out[blockIdx.x] = t1 - t0;
     if (lane < NX) sink[blockIdx.x * 8 + lane] = L.P[lane] + L.dxv[H * NX + lane] + L.K[lane];
     (void)PS;
+}
+
+// correctness: the MFMA4 sweeps against the VALU sweeps on the same stage data
+__device__ void init_stage_data(const KQ::Lds& L, int H, int lane, int salt) {
+    constexpr int NX = KQ::NX, NB = KQ::NB, GS = KQ::GS;
+    if (lane < 8) L.zero[lane] = (lane == 7) ? 1.0 : 0.0;
+    for (int e = lane; e < H * NX * GS; e += 64) {
+        const int j = e % GS, i = (e / GS) % NX;
+        const double r = 0.5 - 0.37 * ((e * 7919) % 101) / 101.0;
+        L.G[e] = (j < NX) ? ((i == j) ? 1.0 : 0.0) + 0.01 * r : (j < NB ? 0.1 * r : 0.01 + 0.02 * r);
+    }
+    for (int e = lane; e < (H + 1) * NB; e += 64) {
+        L.hq[e] = 1.0 + 0.1 * ((e * 31) % 17);
+        L.gq[e] = 0.01 * ((e * (13 + salt)) % 7) - 0.03;
+    }
+    WSYNC();
+    KQ::mfma_backward(L, H, lane);
+    WSYNC();
+    KQ::template acl_phase<true>(L, H, lane);
+    WSYNC();
+}
+
+__global__ __launch_bounds__(64) void cmp(int H, double* out) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const auto L = KQ::carve(smem, H);
+    const int lane = threadIdx.x;
+    constexpr int NX = KQ::NX, NU = KQ::NU, PS = KQ::PS, PP = KQ::PP, PO = KQ::PO;
+    const int nd = (H + 1) * NX, nk = H * NU;
+    auto pval = [&](int e) { return L.P[(e / NX) * PP + PO + e % NX]; };
+    auto kval = [&](int e) { return L.K[(e / NU) * NU * PS + (e % NU) * PS + NX]; };
+    init_stage_data(L, H, lane, 0);
+    KQ::valu_forward(L, H, lane);
+    WSYNC();
+    double a[8];
+    for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; a[q] = e < nd ? L.dxv[e] : 0.0; }
+    WSYNC();
+    KQ::mfma4_forward(L, H, lane);
+    WSYNC();
+    double err = 0.0, mag = 0.0;
+    for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) { err = fmax(err, fabs(L.dxv[e] - a[q])); mag = fmax(mag, fabs(a[q])); } }
+    WSYNC();
+    KQ::mfma4_forward<1>(L, H, lane);
+    WSYNC();
+    for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) err = fmax(err, fabs(L.dxv[e] - a[q])); }
+    WSYNC();
+    // factorisation with the N-form Schur step against the MFMA Schur step: P', K', Ru^-1
+    {
+        constexpr int PPn = KQ::PP;
+        init_stage_data(L, H, lane, 5);
+        double pa[16], ka[8];
+        for (int q = 0; q < 16; ++q) { const int e = lane + 64 * q; pa[q] = e < (H + 1) * PPn ? L.P[e] : 0.0; }
+        for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; ka[q] = e < H * KQ::NU * KQ::PS ? L.K[e] : 0.0; }
+        WSYNC();
+        init_stage_data(L, H, lane, 5);
+        KQ::mfma_backward<true>(L, H, lane);
+        WSYNC();
+        double ef = 0.0, mf = 0.0;
+        for (int q = 0; q < 16; ++q) { const int e = lane + 64 * q; if (e >= PPn && e < (H + 1) * PPn) { ef = fmax(ef, fabs(L.P[e] - pa[q])); mf = fmax(mf, fabs(pa[q])); } }
+        for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < H * KQ::NU * KQ::PS) { ef = fmax(ef, fabs(L.K[e] - ka[q])); mf = fmax(mf, fabs(ka[q])); } }
+        ef = wave_max(ef); mf = wave_max(mf);
+        if (lane == 0) { out[4] = ef; out[5] = mf; }
+    }
+    WSYNC();
+    init_stage_data(L, H, lane, 3);
+    KQ::valu_vector_backward<false>(L, H, lane);
+    double p1[8], k1[4];
+    for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; p1[q] = e < nd ? pval(e) : 0.0; }
+    for (int q = 0; q < 4; ++q) { const int e = lane + 64 * q; k1[q] = e < nk ? kval(e) : 0.0; }
+    WSYNC();
+    init_stage_data(L, H, lane, 3);
+    KQ::valu_vector_backward<true>(L, H, lane);
+    double errp = 0.0, magp = 0.0;
+    for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) { errp = fmax(errp, fabs(pval(e) - p1[q])); magp = fmax(magp, fabs(p1[q])); } }
+    for (int q = 0; q < 4; ++q) { const int e = lane + 64 * q; if (e < nk) { errp = fmax(errp, fabs(kval(e) - k1[q])); magp = fmax(magp, fabs(k1[q])); } }
+    err = wave_max(err); mag = wave_max(mag); errp = wave_max(errp); magp = wave_max(magp);
+    if (lane == 0) { out[0] = err; out[1] = mag; out[2] = errp; out[3] = magp; }
+}
+
+static void check(int H) {
+    double* d;
+    (void)hipMalloc(&d, 6 * sizeof(double));
+    cmp<<<1, 64, KQ::lds_doubles(H) * sizeof(double)>>>(H, d);
+    double h[6];
+    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    printf("check forward mfma4 (both) vs valu: max |diff| %.3e (max |dx| %.3e); vector backward: %.3e (max %.3e); "
+           "factor N-form vs MFMA Schur: %.3e (max %.3e)\n", h[0], h[1], h[2], h[3], h[4], h[5]);
 }
 
 template <int V>
@@ -83,8 +172,12 @@ int main() {
     run<0>("backward (factor)", H, B, reps, d_out, d_sink);
     run<1>("backward (vector)", H, B, reps, d_out, d_sink);
     run<2>("closed-loop maps", H, B, reps, d_out, d_sink);
-    run<3>("forward (mfma)", H, B, reps, d_out, d_sink);
+    run<3>("forward (mfma4)", H, B, reps, d_out, d_sink);
     run<4>("forward (valu)", H, B, reps, d_out, d_sink);
+    run<6>("backward (vec mfma4)", H, B, reps, d_out, d_sink);
+    run<7>("backward (factor, N)", H, B, reps, d_out, d_sink);
+    run<8>("forward (mfma4 2x)", H, B, reps, d_out, d_sink);
     run<5>("wave_sum x H", H, B, reps, d_out, d_sink);
+    check(H);
     return 0;
 }
