@@ -143,6 +143,38 @@ __device__ __forceinline__ double exp_rbf(double x) {
     return __hiloint2double(__double2hiint(p) + (ni << 20), __double2loint(p));
 }
 
+// exp_rbf of K independent arguments, written step by step across the K values.  One wave
+// issues an f64 VALU operation every ~5.5 cycles whether or not it depends on the previous one,
+// but a dependent one waits ~7.3 (tools/probe_f64.hip): the compiler schedules back-to-back
+// exp_rbf calls as K serial 15-deep chains (124 cycles per exp), the interleaved form runs at
+// the issue rate (94 cycles per exp with K = 8).  Same operations, same results as exp_rbf.
+template <int K>
+__device__ __forceinline__ void exp_rbf_n(double (&x)[K]) {
+    constexpr double kMagic = 6755399441055744.0;   // 1.5 * 2^52
+    constexpr double c[12] = {2.5110037605963777e-08, 2.763263963904103e-07, 2.755724091857897e-06,
+                              2.4801485482328494e-05, 0.00019841269890047113, 0.0013888888952314775,
+                              0.008333333333319601, 0.0416666666664881, 0.1666666666666668,
+                              0.5000000000000019, 1.0, 1.0};
+    double t[K], r[K], p[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = fma(x[k], 1.4426950408889634, kMagic);
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = fma(t[k] - kMagic, -6.93147180369123816490e-01, x[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) r[k] = fma(t[k] - kMagic, -1.90821492927058770002e-10, r[k]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) p[k] = fma(c[0], r[k], c[1]);
+#pragma unroll
+    for (int i = 2; i < 12; ++i)
+#pragma unroll
+        for (int k = 0; k < K; ++k) p[k] = fma(p[k], r[k], c[i]);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int ni = max(__double2loint(t[k]), -1022);
+        x[k] = __hiloint2double(__double2hiint(p[k]) + (ni << 20), __double2loint(p[k]));
+    }
+}
+
 // Up to kMaxGP posterior evaluations in one launch (grid.y = GP).
 struct PostBatch {
     GPDev g[kMaxGP];

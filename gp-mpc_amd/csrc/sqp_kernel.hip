@@ -215,15 +215,16 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
     auto finish = [&](const f64x4 (&a)[NE], const Wops& w) {
         auto d = [](unsigned lo, unsigned hi) { return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32)); };
         const double wr[4] = {d(w.a[0], w.a[1]), d(w.a[2], w.a[3]), d(w.b[0], w.b[1]), d(w.b[2], w.b[3])};
-        double ex[NE][4];
+        double ex[NE * 4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int e = 0; e < NE; ++e) ex[e][r] = exp_rbf(a[e][r]);
+            for (int e = 0; e < NE; ++e) ex[e * 4 + r] = a[e][r];
+        exp_rbf_n<NE * 4>(ex);   // all exps of the tile interleaved (issue-bound, not chain-bound)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int e = 0; e < NE; ++e) acc[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(wr[r], ex[e][r], acc[e], 0, 0, 0);
+            for (int e = 0; e < NE; ++e) acc[e] = __builtin_amdgcn_mfma_f64_4x4x4f64(wr[r], ex[e * 4 + r], acc[e], 0, 0, 0);
     };
     // Software pipeline, two tiles per iteration (ping-pong names, no register copies on the
     // back edge): tile t+1's exponent MFMAs are issued before tile t's exps and contraction, so
