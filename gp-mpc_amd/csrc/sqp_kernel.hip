@@ -824,7 +824,9 @@ struct SqpKernel {
     //   Schur onto the state block       Ru by readlane, row/column slices by lane shuffles
     __device__ static int pidx(int i, int j) { return i * NX - (i * (i - 1)) / 2 + (j - i); }  // i <= j < NX
 
-    template <bool kSchurN = false>
+    // DIAG (tools/ric_micro.hip only): bit 0 drops the P', K', Ru^-1 stores, bit 1 replaces the
+    // Ru inverse chain by a plain move (measures the MFMA chain alone).
+    template <bool kSchurN = false, int DIAG = 0>
     __device__ static bool mfma_backward(const Lds& L, int H, int lane) {
         const int lr = lane >> 4, lc = lane & 15;
         const bool colok = (lc < NX) || (lc == NB);
@@ -913,6 +915,22 @@ struct SqpKernel {
         const bool rst = lane < NU * NU;
         double* srui = rst ? L.Rui + (H - 1) * NU * NU + lane : L.dummy + lane;
         const int srui_st = rst ? NU * NU : 0;
+        // DIAG bit 2: the stores of stage k are issued inside stage k-1, after its W' products
+        // (off the recursion's dependency chain), and the K' chain is rcp -> e -> fma -> fma
+        constexpr bool kDefer = (DIAG & 4) != 0;
+        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
+        bool pend = false;
+        auto flush = [&]() {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                *sp[r] = pend_p[r];
+                sp[r] -= sp_st[r];
+            }
+            *sk = pend_k;
+            sk -= sk_st;
+            *srui = pend_r;
+            srui -= srui_st;
+        };
         auto stage = [&](int k, const Stage& sd) {
             // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
             // rows 8..15 of W' are never read (M' takes w[0], w[1]), so their C-init is P'_{k+1}'s own
@@ -922,6 +940,10 @@ struct SqpKernel {
             // the M' product never reads, so it needs no mask)
             f64x4 w = mfma64(pn[0], sd.g[0], cw);
             w = mfma64(pn[1], sd.g[1], w);
+            if constexpr (kDefer) {
+                if (pend) flush();
+                pend = true;
+            }
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], 0.0, 0.0});
             m = mfma64(sd.g[1], w[1], m);
             // Ru = M'_uu by readlane.  K' = -Ru^-1 M'_u through the adjugate: the numerators are
@@ -932,7 +954,8 @@ struct SqpKernel {
             for (int a = 0; a < NU; ++a)
 #pragma unroll
                 for (int b2 = a; b2 < NU; ++b2) {
-                    Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
+                    if constexpr ((DIAG & 2) != 0) Ru[a][b2] = (a == b2) ? 1.0 : 0.0;
+                    else Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
                     Ru[b2][a] = Ru[a][b2];
                 }
             // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry).
@@ -956,18 +979,33 @@ struct SqpKernel {
                 // lane a=0: mu = M'[NX], mo = M'[NX+1]; lane a=1: mu = M'[NX+1], mo = M'[NX]
                 const double mo = xor16_d(mu);
                 num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
-                id = fast_rcp(det);
-                kb = num * -id;
+                if constexpr (kDefer) {
+                    // id = r (1 + e + e^2): kb = t + t (e + e^2) with t = -num r beside e
+                    const double r0 = __builtin_amdgcn_rcp(det);
+                    const double e = fma(-det, r0, 1.0);
+                    const double ee = fma(e, e, e);
+                    const double t = num * -r0;
+                    id = fma(r0, ee, r0);
+                    kb = fma(t, ee, t);
+                } else {
+                    id = fast_rcp(det);
+                    kb = num * -id;
+                }
                 Ri[0][0] = Ru[1][1] * id;
                 Ri[1][1] = Ru[0][0] * id;
                 Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
             }
-            {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
+            if constexpr ((DIAG & 1) == 0) {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
                 double rv = Ri[0][0];
                 if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
-                *srui = rv;
-                srui -= srui_st;
+                if constexpr (kDefer) {
+                    pend_r = rv;
+                } else {
+                    *srui = rv;
+                    srui -= srui_st;
+                }
             }
+            if constexpr ((DIAG & 2) != 0) kb = -mu * 1e-3;
             // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M').  kSchurN: the numerator product
             // N = M'_xu adj(Ru) M'_u runs on the matrix core while det / rcp run on the VALU, and
             // P'_k = M' - N / det is one fma per register (rows 8..15 keep M', finite and unread).
@@ -981,8 +1019,12 @@ struct SqpKernel {
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 // branch-free store: entries that are not stored go to a dummy slot
-                *sp[r] = pk[r];
-                sp[r] -= sp_st[r];
+                if constexpr (kDefer) {
+                    pend_p[r] = pk[r];
+                } else if constexpr ((DIAG & 1) == 0) {
+                    *sp[r] = pk[r];
+                    sp[r] -= sp_st[r];
+                }
                 // P'_k is the next stage's A operand unmasked: its entries outside rows < NX and
                 // columns {< NX, NB} are finite and only reach W' rows the M' product never reads
                 // (u columns / rows >= NB) or meet the zero rows >= NX of the G' operand, so the
@@ -990,8 +1032,12 @@ struct SqpKernel {
                 pn[r] = pk[r];
             }
             pq = pk;
-            *sk = kb;
-            sk -= sk_st;
+            if constexpr (kDefer) {
+                pend_k = kb;
+            } else if constexpr ((DIAG & 1) == 0) {
+                *sk = kb;
+                sk -= sk_st;
+            }
         };
         // stage k's operands are loaded one stage ahead (explicit double buffer: no register
         // copies that would force the wait right after the load)
@@ -1005,6 +1051,185 @@ struct SqpKernel {
             stage(k - 1, s1);
         }
         if (k == 0) stage(0, s0);
+        if constexpr (kDefer) flush();
+        if constexpr ((DIAG & 3) != 0) L.dummy[lane] = pn[0] + pn[1];   // keeps the chain alive without the stores
+        return ok;
+    }
+
+    // Riccati factorisation on v_mfma_f64_16x16x4 in the homogeneous tile layout: tile index t of
+    // the 16-wide operands is x_t for t < NX, the affine "1" at CI = NX, u_a at UI + a (UI = 8),
+    // zero elsewhere.  The affine column c of G'_k becomes row/column CI of [G'_k; e_CI]
+    // (G'' row CI = e_CI, the one slot of the LDS zero block), so W' = P'_{k+1} G'' needs no
+    // C-init from P' (p_{k+1} rides in row CI of P', inside the K range 0..7 of the two MFMAs),
+    // and M' = G''^T W' + D (D: diag(hq), gq in row and column CI) keeps P'_k = Schur(M')
+    // symmetric, so the Schur MFMA's output registers are the next stage's A operand as they
+    // stand: no select or copy between the Schur product and the next W' on the recursion.
+    // The u rows sit at 8..8+NU-1 = lane groups 0..NU-1 of element 2: the Schur A operand needs no
+    // lane move.  Stores of stage k are issued after stage k-1's W' products (sched_barrier), off
+    // the chain.  Outputs identical in format to mfma_backward (packed P', K', Ru^-1).
+    template <int DIAG = 0>
+    __device__ static bool mfma_backward_h(const Lds& L, int H, int lane) {
+        const int lr = lane >> 4, lc = lane & 15;
+        constexpr int CI = NX, UI = 8;
+        static_assert(NX + 1 <= 8 && NU <= 2 && UI + NU <= 16, "homogeneous tile layout");
+        // tile index -> G' column (-1: structurally zero) and stage variable (-1: none)
+        auto gcol = [](int t) { return t < NX ? t : (t == CI ? NB : ((t >= UI && t < UI + NU) ? NX + t - UI : -1)); };
+        auto svar = [](int t) { return t < NX ? t : ((t >= UI && t < UI + NU) ? NX + t - UI : -1); };
+        const int gc_lc = gcol(lc), sv_lc = svar(lc);
+        double pn[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {   // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
+            const int t = lr + 4 * r;
+            double v = 0.0;
+            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
+            else if (t < NX && lc == CI) v = L.gq[H * NB + t];
+            else if (t == CI && lc < NX) v = L.gq[H * NB + lc];
+            pn[r] = v;
+        }
+        {   // P'_H (packed) for the multiplier recovery of stage H-1
+            double* PH = L.P + (size_t)H * PP;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int t = lr + 4 * r;
+                if (t < NX) {
+                    if (lc == CI) PH[PO + t] = pn[r];
+                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
+                }
+            }
+        }
+        bool ok = true;
+        // G'' rows 4s + lr (K index), column lc: per-lane (base, stride) streams
+        const double* pg[2];
+        int gst[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int t = lr + 4 * s2;
+            const bool ld = t < NX && gc_lc >= 0;
+            const bool one = t == CI && lc == CI;
+            pg[s2] = ld ? L.G + (size_t)(H - 1) * NX * GS + t * GS + gc_lc : L.zero + (one ? 7 : 0);
+            gst[s2] = ld ? NX * GS : 0;
+        }
+        // C-init of M' (rows lr + 4r, r = 0..2): hq on the diagonal, gq in row and column CI
+        const double* pd[3];
+        int dst[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int t = lr + 4 * r, sv_t = svar(t);
+            const double* base = L.zero;
+            bool on = false;
+            if (sv_t >= 0 && t == lc) { base = L.hq + sv_t; on = true; }
+            else if (sv_t >= 0 && lc == CI) { base = L.gq + sv_t; on = true; }
+            else if (t == CI && sv_lc >= 0) { base = L.gq + sv_lc; on = true; }
+            pd[r] = on ? base + (size_t)(H - 1) * NB : L.zero;
+            dst[r] = on ? NB : 0;
+        }
+        struct Stage { double g[2], d[3]; };
+        auto load_stage = [&](Stage& st) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                st.g[q] = *pg[q];
+                pg[q] -= gst[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                st.d[q] = *pd[q];
+                pd[q] -= dst[q];
+            }
+        };
+        // store streams (stages H-1 .. 0), dummy slot with stride 0 for entries not stored
+        double* sp[2];
+        int sp_st[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int t = lr + 4 * r;
+            const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc));
+            const int idx = (lc == CI) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
+            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy + lane;
+            sp_st[r] = st ? PP : 0;
+        }
+        const bool kst = lr < NU && (lc < NX || lc == CI);
+        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + (lc == CI ? NX : lc) : L.dummy + lane;
+        const int sk_st = kst ? NU * PS : 0;
+        const bool rst = lane < NU * NU;
+        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lane : L.dummy + lane;
+        const int srui_st = rst ? NU * NU : 0;
+        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
+        bool pend = false;
+        auto flush = [&]() {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                *sp[r] = pend_p[r];
+                sp[r] -= sp_st[r];
+            }
+            *sk = pend_k;
+            sk -= sk_st;
+            *srui = pend_r;
+            srui -= srui_st;
+        };
+        auto stage = [&](const Stage& sd) {
+            f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
+            w = mfma64(pn[1], sd.g[1], w);
+            if constexpr ((DIAG & 1) == 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (pend) flush();
+                __builtin_amdgcn_sched_barrier(0);
+                pend = true;
+            }
+            f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
+            m = mfma64(sd.g[1], w[1], m);
+            double Ru[NU][NU];
+#pragma unroll
+            for (int a = 0; a < NU; ++a)
+#pragma unroll
+                for (int b2 = a; b2 < NU; ++b2) {
+                    Ru[a][b2] = readlane_d(m[2], (a << 4) | (UI + b2));
+                    Ru[b2][a] = Ru[a][b2];
+                }
+            const double mu = m[2];   // lane (a, c) <- M'[UI + a][c]
+            double kb, Ri[NU][NU];
+            if constexpr (NU == 1) {
+                ok = ok && (Ru[0][0] > 0.0);
+                const double id = fast_rcp(Ru[0][0]);
+                Ri[0][0] = id;
+                kb = -id * mu;
+            } else {
+                const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
+                ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
+                const double mo = xor16_d(mu);
+                const double num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
+                // id = r (1 + e + e^2): kb = t + t (e + e^2) with t = -num r formed beside e
+                const double r0 = __builtin_amdgcn_rcp(det);
+                const double e = fma(-det, r0, 1.0);
+                const double ee = fma(e, e, e);
+                const double t = num * -r0;
+                const double id = fma(r0, ee, r0);
+                kb = fma(t, ee, t);
+                Ri[0][0] = Ru[1][1] * id;
+                Ri[1][1] = Ru[0][0] * id;
+                Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
+            }
+            const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);   // P'_k = M' + M'_{.u} K'
+            double rv = Ri[0][0];
+            if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
+            pend_p[0] = pk[0];
+            pend_p[1] = pk[1];
+            pend_k = kb;
+            pend_r = rv;
+            pn[0] = pk[0];
+            pn[1] = pk[1];
+        };
+        Stage s0, s1;
+        load_stage(s0);
+        int k = H - 1;
+        for (; k >= 1; k -= 2) {
+            load_stage(s1);
+            stage(s0);
+            if (k >= 2) load_stage(s0);
+            stage(s1);
+        }
+        if (k == 0) stage(s0);
+        if constexpr ((DIAG & 1) == 0) flush();
+        else L.dummy[lane] = pn[0] + pn[1];
         return ok;
     }
 
@@ -1773,7 +1998,7 @@ struct SqpKernel {
                     TPHASE(4);
                     double dd[NV], dp[NX];
                     if constexpr (kMfma) {
-                        if (!mfma_backward(L, H, lane)) { qp_ok = false; break; }
+                        if (!mfma_backward_h(L, H, lane)) { qp_ok = false; break; }
                         WSYNC();
                         TPHASE(8);
                         acl_phase<true>(L, H, lane);

@@ -38,6 +38,11 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     for (int r = 0; r < reps; ++r) {
         if constexpr (V == 0) KQ::mfma_backward(L, H, lane);
         if constexpr (V == 7) KQ::mfma_backward<true>(L, H, lane);
+        if constexpr (V == 9) KQ::mfma_backward<false, 1>(L, H, lane);
+        if constexpr (V == 10) KQ::mfma_backward<false, 3>(L, H, lane);
+        if constexpr (V == 11) KQ::mfma_backward<false, 4>(L, H, lane);
+        if constexpr (V == 12) KQ::mfma_backward_h(L, H, lane);
+        if constexpr (V == 13) KQ::mfma_backward_h<1>(L, H, lane);
         if constexpr (V == 8) KQ::mfma4_forward<1>(L, H, lane);
         if constexpr (V == 1) KQ::valu_vector_backward(L, H, lane);
         if constexpr (V == 2) KQ::template acl_phase<true>(L, H, lane);
@@ -105,7 +110,9 @@ __global__ __launch_bounds__(64) void cmp(int H, double* out) {
         for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; ka[q] = e < H * KQ::NU * KQ::PS ? L.K[e] : 0.0; }
         WSYNC();
         init_stage_data(L, H, lane, 5);
-        KQ::mfma_backward<true>(L, H, lane);
+        if (out[6] > 1.5) KQ::mfma_backward_h(L, H, lane);
+        else if (out[6] > 0.5) KQ::mfma_backward<false, 4>(L, H, lane);
+        else KQ::mfma_backward<true>(L, H, lane);
         WSYNC();
         double ef = 0.0, mf = 0.0;
         for (int q = 0; q < 16; ++q) { const int e = lane + 64 * q; if (e >= PPn && e < (H + 1) * PPn) { ef = fmax(ef, fabs(L.P[e] - pa[q])); mf = fmax(mf, fabs(pa[q])); } }
@@ -131,12 +138,17 @@ __global__ __launch_bounds__(64) void cmp(int H, double* out) {
 
 static void check(int H) {
     double* d;
-    (void)hipMalloc(&d, 6 * sizeof(double));
-    cmp<<<1, 64, KQ::lds_doubles(H) * sizeof(double)>>>(H, d);
-    double h[6];
-    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    printf("check forward mfma4 (both) vs valu: max |diff| %.3e (max |dx| %.3e); vector backward: %.3e (max %.3e); "
-           "factor N-form vs MFMA Schur: %.3e (max %.3e)\n", h[0], h[1], h[2], h[3], h[4], h[5]);
+    (void)hipMalloc(&d, 7 * sizeof(double));
+    for (int variant = 0; variant < 3; ++variant) {
+        const double flag = variant;
+        (void)hipMemcpy(d + 6, &flag, sizeof(double), hipMemcpyHostToDevice);
+        cmp<<<1, 64, KQ::lds_doubles(H) * sizeof(double)>>>(H, d);
+        double h[6];
+        (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+        printf("check forward mfma4 (both) vs valu: max |diff| %.3e (max |dx| %.3e); vector backward: %.3e (max %.3e); "
+               "factor %s vs MFMA Schur: %.3e (max %.3e)\n", h[0], h[1], h[2], h[3],
+               variant == 2 ? "homogeneous" : (variant ? "deferred-store" : "N-form"), h[4], h[5]);
+    }
 }
 
 template <int V>
@@ -178,6 +190,11 @@ int main() {
     run<7>("backward (factor, N)", H, B, reps, d_out, d_sink);
     run<8>("forward (mfma4 2x)", H, B, reps, d_out, d_sink);
     run<5>("wave_sum x H", H, B, reps, d_out, d_sink);
+    run<9>("factor, no stores", H, B, reps, d_out, d_sink);
+    run<10>("factor, MFMA chain", H, B, reps, d_out, d_sink);
+    run<11>("factor, deferred st", H, B, reps, d_out, d_sink);
+    run<12>("factor, homogeneous", H, B, reps, d_out, d_sink);
+    run<13>("factor, homog no st", H, B, reps, d_out, d_sink);
     check(H);
     return 0;
 }
