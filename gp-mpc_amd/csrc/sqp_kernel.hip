@@ -1233,6 +1233,182 @@ struct SqpKernel {
         return ok;
     }
 
+    // ------------------------------------------------------------------ Riccati on MFMA, NX <= 12, NU <= 4
+    // For stages wider than one 16x16 tile (quad3d: NX = 12, NU = 4, NB + 1 = 17) the products are
+    // split over two column tiles of v_mfma_f64_16x16x4_f64: T1 = [x | c] (c at tile column NX) and
+    // T2 = u.  With P' = [P | p] in the C layout (rows 0..NX-1 in elements 0..KS-1, p in column NX):
+    //   W1 = P' [G'_x | c] + p e_NX      W2 = P' G'_u                       (KS chained MFMAs each)
+    //   M11 = T1^T W1 + [diag(hq_x) | gq_x]   M21 = T2^T W1 + [0 | gq_u]   M22 = T2^T W2 + diag(hq_u)
+    //   Ru = M22 (readlane), Ru^-1 by 2x2 blocks (two reciprocals), K' = -Ru^-1 M21 per lane from the
+    //   four u rows of its column (permlane16/32 swaps), P'_k = M11 + M21^T K' (one MFMA).
+    // M21's element 0 (lane (a, j) = M21[a][j]) is both the Schur product's A operand and the
+    // right-hand side of K'.  Replaces the VALU riccati_factor (LDS round trips per product) for
+    // quad3d; outputs in its format (packed P', K', Ru^-1).
+    static constexpr bool kMfmaBig = !kMfma && NX <= 12 && NX + 1 <= 16 && NU == 4;
+    __device__ static bool mfma_backward_big(const Lds& L, int H, int lane) {
+        if constexpr (!kMfmaBig) {
+            return false;
+        } else {
+        const int lr = lane >> 4, lc = lane & 15;
+        constexpr int KS = (NX + 3) / 4;   // K steps over the state rows
+        double pn[KS];
+#pragma unroll
+        for (int r = 0; r < KS; ++r) {   // P'_H = [diag(hq_H[x]) | gq_H[x]]
+            const int t = lr + 4 * r;
+            double v = 0.0;
+            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
+            else if (t < NX && lc == NX) v = L.gq[H * NB + t];
+            pn[r] = v;
+        }
+        {
+            double* PH = L.P + (size_t)H * PP;
+#pragma unroll
+            for (int r = 0; r < KS; ++r) {
+                const int t = lr + 4 * r;
+                if (t < NX) {
+                    if (lc == NX) PH[PO + t] = pn[r];
+                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
+                }
+            }
+        }
+        bool ok = true;
+        // stage operand streams (stages H-1 .. 0)
+        const double* pa[KS];   // T1 = [G'_x | c]: row 4s + lr, tile column lc
+        const double* pb[KS];   // T2 = G'_u
+        int ast[KS], bst[KS];
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const int t = lr + 4 * s2;
+            const bool la = t < NX && lc <= NX;
+            const bool lb = t < NX && lc < NU;
+            pa[s2] = la ? L.G + (size_t)(H - 1) * NX * GS + t * GS + (lc < NX ? lc : NB) : L.zero;
+            pb[s2] = lb ? L.G + (size_t)(H - 1) * NX * GS + t * GS + NX + lc : L.zero;
+            ast[s2] = la ? NX * GS : 0;
+            bst[s2] = lb ? NX * GS : 0;
+        }
+        const double* pd11[KS];   // M11 C-init: hq_x on the diagonal, gq_x in column NX
+        int d11st[KS];
+#pragma unroll
+        for (int r = 0; r < KS; ++r) {
+            const int t = lr + 4 * r;
+            const bool dg = t < NX && t == lc, gc = t < NX && lc == NX;
+            pd11[r] = dg ? L.hq + (size_t)(H - 1) * NB + t : (gc ? L.gq + (size_t)(H - 1) * NB + t : L.zero);
+            d11st[r] = (dg || gc) ? NB : 0;
+        }
+        const bool g21 = lr < NU && lc == NX, d22 = lr < NU && lc == lr;
+        const double* pd21 = g21 ? L.gq + (size_t)(H - 1) * NB + NX + lr : L.zero;
+        const double* pd22 = d22 ? L.hq + (size_t)(H - 1) * NB + NX + lr : L.zero;
+        const int d21st = g21 ? NB : 0, d22st = d22 ? NB : 0;
+        struct Stage { double a[KS], b[KS], d11[KS], d21, d22; };
+        auto load_stage = [&](Stage& st) {
+#pragma unroll
+            for (int q = 0; q < KS; ++q) {
+                st.a[q] = *pa[q];
+                pa[q] -= ast[q];
+                st.b[q] = *pb[q];
+                pb[q] -= bst[q];
+                st.d11[q] = *pd11[q];
+                pd11[q] -= d11st[q];
+            }
+            st.d21 = *pd21;
+            pd21 -= d21st;
+            st.d22 = *pd22;
+            pd22 -= d22st;
+        };
+        // store streams
+        double* sp[KS];
+        int sp_st[KS];
+#pragma unroll
+        for (int r = 0; r < KS; ++r) {
+            const int t = lr + 4 * r;
+            const bool st = t < NX && ((lc == NX) || (lc < NX && t <= lc));
+            const int idx = (lc == NX) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
+            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy + lane;
+            sp_st[r] = st ? PP : 0;
+        }
+        const bool kst = lr < NU && lc <= NX;
+        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + lc : L.dummy + lane;
+        const int sk_st = kst ? NU * PS : 0;
+        const bool rst = lr < NU && lc < NU;
+        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lr * NU + lc : L.dummy + lane;
+        const int srui_st = rst ? NU * NU : 0;
+        auto stage = [&](const Stage& sd) {
+            f64x4 w1 = {0.0, 0.0, 0.0, 0.0}, w2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < KS; ++r) w1[r] = (lc == NX) ? pn[r] : 0.0;
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                w1 = mfma64(pn[s2], sd.a[s2], w1);
+                w2 = mfma64(pn[s2], sd.b[s2], w2);
+            }
+            f64x4 m22 = {sd.d22, 0.0, 0.0, 0.0}, m21 = {sd.d21, 0.0, 0.0, 0.0}, m11 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int r = 0; r < KS; ++r) m11[r] = sd.d11[r];
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                m22 = mfma64(sd.b[s2], w2[s2], m22);
+                m21 = mfma64(sd.b[s2], w1[s2], m21);
+                m11 = mfma64(sd.a[s2], w1[s2], m11);
+            }
+            // Ru = M22[0..3][0..3] and its inverse by 2x2 blocks [[A, B], [B^T, C]]
+            const double mz = m22[0];
+            const double a00 = readlane_d(mz, 0), a01 = readlane_d(mz, 1), a11 = readlane_d(mz, 16 + 1);
+            const double b00 = readlane_d(mz, 2), b01 = readlane_d(mz, 3), b10 = readlane_d(mz, 16 + 2),
+                         b11 = readlane_d(mz, 16 + 3);
+            const double c00 = readlane_d(mz, 32 + 2), c01 = readlane_d(mz, 32 + 3), c11 = readlane_d(mz, 48 + 3);
+            const double dA = fma(a00, a11, -a01 * a01);
+            const double iA = fast_rcp(dA);
+            const double A00 = a11 * iA, A01 = -a01 * iA, A11 = a00 * iA;
+            const double X00 = fma(A00, b00, A01 * b10), X01 = fma(A00, b01, A01 * b11);
+            const double X10 = fma(A01, b00, A11 * b10), X11 = fma(A01, b01, A11 * b11);
+            const double S00 = c00 - fma(b00, X00, b10 * X10), S01 = c01 - fma(b00, X01, b10 * X11);
+            const double S11 = c11 - fma(b01, X01, b11 * X11);
+            const double dS = fma(S00, S11, -S01 * S01);
+            ok = ok && (a00 > 0.0) && (dA > 0.0) && (dS > 0.0);
+            const double iS = fast_rcp(dS);
+            const double C00 = S11 * iS, C01 = -S01 * iS, C11 = S00 * iS;
+            const double Y00 = fma(X00, C00, X01 * C01), Y01 = fma(X00, C01, X01 * C11);
+            const double Y10 = fma(X10, C00, X11 * C01), Y11 = fma(X10, C01, X11 * C11);
+            const double Z00 = A00 + fma(Y00, X00, Y01 * X01), Z01 = A01 + fma(Y00, X10, Y01 * X11);
+            const double Z11 = A11 + fma(Y10, X10, Y11 * X11);
+            // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a, column a ^ t, for lane group a
+            const int a = lr;
+            const double c0 = (a == 0) ? Z00 : ((a == 1) ? Z11 : ((a == 2) ? C00 : C11));
+            const double c1 = (a & 2) ? C01 : Z01;
+            const double c2 = (a & 1) ? -Y11 : -Y00;                  // (0,2) = -Y00, (1,3) = -Y11
+            const double c3 = ((a ^ (a >> 1)) & 1) ? -Y10 : -Y01;    // (0,3) = -Y01, (1,2) = -Y10
+            // the four u rows of this lane's column of M21 (lane group b holds row b)
+            const double v0 = m21[0], v1 = xor16_d(v0), v2 = xor32_d(v0), v3 = xor32_d(v1);
+            const double kb = -fma(c0, v0, fma(c1, v1, fma(c2, v2, c3 * v3)));
+            const f64x4 pk = mfma64(lr < NU ? v0 : 0.0, kb, m11);   // P'_k = M11 + M21^T K'
+            // stores: P' (packed), K' (feedback + kff), Ru^-1 (lane (a, c): column c = a ^ t)
+            const int t = lc ^ a;
+            const double rv = (t == 0) ? c0 : ((t == 1) ? c1 : ((t == 2) ? c2 : c3));
+#pragma unroll
+            for (int r = 0; r < KS; ++r) {
+                *sp[r] = pk[r];
+                sp[r] -= sp_st[r];
+                pn[r] = pk[r];
+            }
+            *sk = kb;
+            sk -= sk_st;
+            *srui = rv;
+            srui -= srui_st;
+        };
+        Stage s0, s1;
+        load_stage(s0);
+        int k = H - 1;
+        for (; k >= 1; k -= 2) {
+            load_stage(s1);
+            stage(s0);
+            if (k >= 2) load_stage(s0);
+            stage(s1);
+        }
+        if (k == 0) stage(s0);
+        return ok;
+        }
+    }
+
     // Closed-loop stage maps A'_k = [A + B K | B kff + c] (all stages in parallel); only the
     // affine column when the factorisation is unchanged (corrector).
     template <bool full>
@@ -2014,7 +2190,12 @@ struct SqpKernel {
                         recover_q<NV>(L, H, kq, vb, dd, dp);
                         TPHASE(3);
                     } else {
-                        if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
+                        if constexpr (kMfmaBig) {
+                            if (!mfma_backward_big(L, H, lane)) { qp_ok = false; break; }
+                            WSYNC();
+                        } else {
+                            if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
+                        }
                         TPHASE(6);
                         riccati_forward(L, H, lane);
                         TPHASE(3);

@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--no-gp", action="store_true", help="nominal dynamics (isolates the GP sums)")
+    ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5)")
+    ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference")
     args = ap.parse_args()
     from gpmpc import _lib
     from gpmpc.gp import GaussianProcess
@@ -41,6 +43,8 @@ def main():
     from gpmpc.synthetic import DEFAULT_HYPERS, initial_states, make_training_data
 
     spec = get_spec(args.model)
+    if args.var_inputs == "dynamics":
+        spec.var_inputs = spec.gp_inputs
     H, B, N = args.horizon, args.batch, args.n_train
     data = make_training_data(spec, N, seed=1)
     gps = []
@@ -54,7 +58,16 @@ def main():
     if args.no_gp:
         s.set_gps(None)
     else:
-        s.set_gps(gps)
+        fitc = None
+        if args.fitc:
+            from gpmpc.gpmpc import GPMPC
+
+            for gp in gps:
+                gp.K, gp.K_inv = gp.compute_covariances()
+            me = type("Me", (), {})()
+            me.gaussian_process, me.np_random = gps, np.random.default_rng(1337)
+            fitc = GPMPC.precompute_sparse_posterior_mean(me, min(args.fitc, N))
+        s.set_gps(gps, fitc=fitc)
         s.set_tightening(True, 0.95, *mats)
     s.reset(True)
     tbuf = torch.zeros(B, len(PHASES), dtype=torch.int64, device="cuda")
