@@ -28,7 +28,22 @@
 
 namespace gpmpc {
 
-#define WSYNC() __syncthreads()  // block == one wavefront: orders LDS traffic of the wave
+// Orders the LDS traffic of the (main) wave.  One wave per block: __syncthreads.  With GP helper
+// waves (SqpKernel::NWAVES > 1) only the tile passes synchronise the block (B1/B2 in eval_gps and
+// helper_loop); everywhere else the main wave orders its own LDS traffic: a wave's LDS operations
+// execute in issue order, so a wavefront-scope fence (compiler ordering + lgkmcnt wait) suffices.
+template <int NW>
+__device__ __forceinline__ void wave_sync() {
+    if constexpr (NW == 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+#define WSYNC() wave_sync<NWAVES>()
 
 // Diagnostic phase timing (build with -DGPMPC_TIMING): shader-clock cycles per phase,
 // accumulated by the wave and stored per instance.  Phases (kPhases): 0 tightening, 1 linearise,
@@ -183,9 +198,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, int b
     return __builtin_amdgcn_make_buffer_rsrc(u, 0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-template <int NE>
+// TS > 1: this wave takes the tiles t0, t0 + TS, t0 + 2 TS, ... (the GP helper waves of a
+// multi-wave instance, SqpKernel::NWAVES); its partial sums go to `out`.
+template <int NE, int TS = 1>
 __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int nt, const double* zb,
-                                         const double* czzb, double* out, int lane) {
+                                         const double* czzb, double* out, int lane, int t0 = 0) {
     const int lr = lane >> 4, lc = lane & 15;
     double zo[NE], czz[NE];
 #pragma unroll
@@ -202,8 +219,9 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(tX, nt * 64 * 8);
     const __amdgpu_buffer_rsrc_t rw = make_rsrc(tW, nt * 64 * 8);
     const int ox = (lc * 4 + lr) * 8, ow = (lr * 4 + (lc & 3)) * 32;
-    auto ldx = [&](int t) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, ox + t * 512, 0, 0)); };
-    auto ldw = [&](int t, int h) { return __builtin_amdgcn_raw_buffer_load_b128(rw, ow + t * 512 + 16 * h, 0, 0); };
+    // i-th tile of this wave: t0 + i TS (reads past the pack return zeros)
+    auto ldx = [&](int i) { return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, ox + (t0 + i * TS) * 512, 0, 0)); };
+    auto ldw = [&](int i, int h) { return __builtin_amdgcn_raw_buffer_load_b128(rw, ow + (t0 + i * TS) * 512 + 16 * h, 0, 0); };
     struct Wops { decltype(ldw(0, 0)) a, b; };
     auto loadw = [&](int t, Wops& w) { w.a = ldw(t, 0); w.b = ldw(t, 1); };
     // exponent tile of training tile t (one MFMA per evaluation tile)
@@ -231,6 +249,7 @@ __device__ __forceinline__ void gp_tiles(const double* tX, const double* tW, int
     // they run under that VALU work; X operands are fetched two tiles ahead, W one tile ahead.
     // The loop body is one basic block: tiles past nt read zeros (buffer range), whose exponent
     // is finite and whose weights contribute nothing.
+    nt = TS == 1 ? nt : (nt - t0 + TS - 1) / TS;   // tiles of this wave
     double x0 = ldx(0), x1 = ldx(1);
     Wops w0, w1;
     loadw(0, w0);
@@ -263,19 +282,20 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // One copy of the tile loop per evaluation-tile count, shared by every call site (noinline).
 // Three or four evaluation tiles (H > 32) run as two passes to bound the register footprint.
+template <int TS = 1>
 __device__ __attribute__((noinline)) void gp_tiles_dispatch(const double* tX, const double* tW, int ntile,
                                                           const double* zb, const double* czz, double* out,
-                                                          int lane, int ne) {
+                                                          int lane, int ne, int t0 = 0) {
     switch (ne) {
-        case 1: gp_tiles<1>(tX, tW, ntile, zb, czz, out, lane); break;
-        case 2: gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane); break;
+        case 1: gp_tiles<1, TS>(tX, tW, ntile, zb, czz, out, lane, t0); break;
+        case 2: gp_tiles<2, TS>(tX, tW, ntile, zb, czz, out, lane, t0); break;
         case 3:
-            gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane);
-            gp_tiles<1>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane);
+            gp_tiles<2, TS>(tX, tW, ntile, zb, czz, out, lane, t0);
+            gp_tiles<1, TS>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane, t0);
             break;
         default:
-            gp_tiles<2>(tX, tW, ntile, zb, czz, out, lane);
-            gp_tiles<2>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane);
+            gp_tiles<2, TS>(tX, tW, ntile, zb, czz, out, lane, t0);
+            gp_tiles<2, TS>(tX, tW, ntile, zb + 32 * 4, czz + 32, out + 32 * 4, lane, t0);
             break;
     }
 }
@@ -298,18 +318,26 @@ struct SqpKernel {
     // Riccati on v_mfma_f64_16x16x4 when every stage product fits one 16x16 tile
     // (G' has NB+1 <= 16 columns, the forward state [dx; 1] has NX+1 <= 8 rows).
     static constexpr bool kMfma = (NB + 1 <= 16) && (NX + 1 <= 8);
+    // Waves per instance.  The wide model (quad3d) needs more LDS than two instances per CU can
+    // have, so its CU's other SIMDs would idle: three GP helper waves take a share of every GP
+    // tile pass (gp_tiles over tiles w, w + 4, ...), the main wave runs everything else.
+    static constexpr int NWAVES = (NB + 1 > 16) ? 4 : 1;
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
+        int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
     // GP evaluation scratch of the linearisation: points [NGP][16*NE][4], c|z|^2 [NGP][16*NE], sums
     // [NGP][16*NE][4].  It aliases
     // the P' region, which is dead between the QP solves.
-    __host__ __device__ static size_t gp_scratch(int H) { return (size_t)9 * NGP * 16 * ((H + 15) / 16); }
+    __host__ __device__ static size_t gp_scratch(int H) {
+        // + the helper waves' partial sums [NWAVES-1][16*NE][4]
+        return (size_t)9 * NGP * 16 * ((H + 15) / 16) + (size_t)(NWAVES - 1) * 64 * ((H + 15) / 16);
+    }
     __host__ __device__ static size_t p_region(int H) {
         const size_t pp = (size_t)(H + 1) * PP;
         return pp > gp_scratch(H) ? pp : gp_scratch(H);
@@ -317,6 +345,7 @@ struct SqpKernel {
     __host__ __device__ static size_t lds_doubles(int H) {
         const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
                               + (size_t)8                    // zero slots (branch-free masked loads)
+                              + (size_t)8                    // GP helper command slot
                               + (size_t)H * NX * GS            // G'_k
                               + (size_t)H * NU * PS          // K'_k
                               + (size_t)H * NU * NU          // Ru_k^-1
@@ -334,6 +363,7 @@ struct SqpKernel {
         Lds L{};
         L.dummy = s; s += 64;
         L.zero = s;  s += 8;
+        L.ctrl = reinterpret_cast<int*>(s);  s += 8;
         L.G = s;   s += (size_t)H * NX * GS;
         L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
@@ -343,6 +373,7 @@ struct SqpKernel {
         L.gz = s;
         L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
+        L.gsh = L.gs + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         if (kMfma) {
             L.P = s;   s += p_region(H);
             L.Acl = s;
@@ -412,7 +443,21 @@ struct SqpKernel {
             double* zb = L.gz + (size_t)G * np * 4;
             double* cz = L.gc + G * np;
             double* so = L.gs + (size_t)G * np * 4;
-            gp_tiles_dispatch(g.tX, g.tW, g.ntile, zb, cz, so, lane, ne);
+            if constexpr (NWAVES == 1) {
+                gp_tiles_dispatch(g.tX, g.tW, g.ntile, zb, cz, so, lane, ne);
+            } else {
+                // the helper waves take tiles 1, 2, 3 (mod 4) of this pass (helper_loop)
+                if (lane == 0) L.ctrl[0] = G;
+                __syncthreads();   // B1: points and command visible to every wave
+                gp_tiles_dispatch<NWAVES>(g.tX, g.tW, g.ntile, zb, cz, so, lane, ne, 0);
+                __syncthreads();   // B2: partial sums of every wave written
+                for (int e = lane; e < np * 4; e += 64) {
+                    double v = so[e];
+#pragma unroll
+                    for (int w = 1; w < NWAVES; ++w) v += L.gsh[(size_t)(w - 1) * np * 4 + e];
+                    so[e] = v;
+                }
+            }
         });
         WSYNC();
         // 3. mean sf2 S0 and input gradient sf2/ell^2 (S_{1+d} - (z_d - xbar_d) S0) of this lane's stage
@@ -1873,15 +1918,42 @@ struct SqpKernel {
         return (lane < H) ? P.cost_scale * P.r[v - NX] : 1.0;
     }
 
+    // GP helper wave w (1..NWAVES-1): waits for the main wave's tile passes (B1), runs its share
+    // of the pass's tiles into its partial buffer, and meets the main wave again (B2); the main wave
+    // ends the loop with command -1 at the end of the kernel (one more B1).
+    __device__ static void helper_loop(const ProblemDev& P, const Lds& L, int w, int lane) {
+        const int H = P.H;
+        const int ne = (H + 15) >> 4, np = 16 * ne;
+        for (;;) {
+            __syncthreads();   // B1
+            const int G = L.ctrl[0];
+            if (G < 0) break;
+            static_for<NGP>([&](auto gi) {   // static index into the kernel-argument GP array
+                constexpr int GG = decltype(gi)::value;
+                if (GG != G) return;
+                const GPDev& g = P.gp[GG];
+                gp_tiles_dispatch<NWAVES>(g.tX, g.tW, g.ntile, L.gz + (size_t)GG * np * 4, L.gc + (size_t)GG * np,
+                                          L.gsh + (size_t)(w - 1) * np * 4, lane, ne, w);
+            });
+            __syncthreads();   // B2
+        }
+    }
+
     // ------------------------------------------------------------------ the kernel body
     // SPL: the QP's per-variable state is split over two lanes per stage (needs H + 1 <= 32)
     template <bool SPL>
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
-        const int lane = threadIdx.x;
+        const int lane = threadIdx.x & 63;
         const int b = blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve(smem, H);
+        if constexpr (NWAVES > 1) {
+            if (threadIdx.x >= 64) {   // GP helper wave
+                helper_loop(P, L, threadIdx.x >> 6, lane);
+                return;
+            }
+        }
         if (lane < 8) L.zero[lane] = (lane == 7) ? 1.0 : 0.0;   // read by the masked stage-operand streams (7: one)
         const bool on = lane <= H;
         const bool act_x = on && lane >= 1;
@@ -2378,6 +2450,10 @@ struct SqpKernel {
                 for (int i = 0; i < NX; ++i) pi_g[i] = 0.0;
             }
         }
+        if constexpr (NWAVES > 1) {   // release the GP helper waves
+            if (lane == 0) L.ctrl[0] = -1;
+            __syncthreads();   // B1
+        }
         if (lane == 0) {
 #pragma unroll
             for (int a = 0; a < NU; ++a) io.u0[(size_t)b * NU + a] = good ? w[NX + a] : uo[a];
@@ -2433,7 +2509,7 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
 }
 
 template <int ID, bool SPL>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
+__global__ __launch_bounds__(64 * SqpKernel<ID>::NWAVES) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
     SqpKernel<ID>::template run<SPL>(P, S, io);
 }
 
@@ -2445,7 +2521,7 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((sqp_step_kernel<ID, SPL>), dim3(batch), dim3(64), lds, stream, P, S, io);
+    hipLaunchKernelGGL((sqp_step_kernel<ID, SPL>), dim3(batch), dim3(64 * SqpKernel<ID>::NWAVES), lds, stream, P, S, io);
     return hipGetLastError();
 }
 
