@@ -1,16 +1,21 @@
 #!/bin/bash
 # End-of-round evidence on one MI355X (run through gpurun from the repo root):
 #   bash tools/round_profile.sh OUTDIR
-# 1. bench.py (default N=1 line incl. the CPU baseline)   2. rocprofv3 kernel trace/stats + PMC passes
-# 3. in-kernel phase breakdown (timing build)   4. the other BASELINE configs (one shard per GPU)
+# 1. the driver's own command (bench.py --gpus 1 --steps 20 --warmup 5, with the CPU baseline),
+#    rocprofv3 kernel trace/stats, one SQ PMC pass and the FETCH_SIZE / WRITE_SIZE passes of the
+#    same command (tools/driver_prof.sh)
+# 2. in-kernel phase breakdown (timing build) of configs 3 and 5
+# 3. the other BASELINE configs (one shard per GPU), each with its CPU baseline (1 core, all cores)
 set -e
 OUT=${1:?outdir}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p "$OUT"
-timeout -k 10 240 python3 -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
-bash tools/gpu_prof.sh "$OUT/prof"
-timeout -k 10 120 python3 tools/phase_timing.py > "$OUT/phase_timing.txt" 2>&1
-timeout -k 10 180 python3 -u bench.py --no-cpu-baseline --model cartpole --n-train 50 --horizon 20 --batch 256 > "$OUT/config2.json" 2>> "$OUT/bench.err"
-timeout -k 10 180 python3 -u bench.py --no-cpu-baseline --n-train 1000 > "$OUT/config4.json" 2>> "$OUT/bench.err"
-timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
-    --var-inputs dynamics --steps 30 --warmup 5 > "$OUT/config5.json" 2>> "$OUT/bench.err"
+bash tools/driver_prof.sh "$OUT/driver"
+timeout -k 10 120 python3 tools/phase_timing.py --warmup 5 > "$OUT/phase_timing.txt" 2>&1
+timeout -k 10 300 python3 tools/phase_timing.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
+    --var-inputs dynamics --warmup 3 --steps 3 > "$OUT/phase_timing_config5.txt" 2>&1
+timeout -k 10 240 python3 -u bench.py --model cartpole --n-train 50 --horizon 20 --batch 256 \
+    --steps 20 --warmup 5 > "$OUT/config2.json" 2>> "$OUT/bench.err"
+timeout -k 10 300 python3 -u bench.py --n-train 1000 --steps 20 --warmup 5 > "$OUT/config4.json" 2>> "$OUT/bench.err"
+timeout -k 10 600 python3 -u bench.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
+    --var-inputs dynamics --steps 20 --warmup 5 > "$OUT/config5.json" 2>> "$OUT/bench.err"
