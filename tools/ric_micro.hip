@@ -9,6 +9,9 @@
 
 #include "sqp_kernel.hip"
 
+#undef WSYNC
+#define WSYNC() __syncthreads()   // the micro-benchmark kernels are one wave per block
+
 using namespace gpmpc;
 using KQ = SqpKernel<kQuad2D>;
 
