@@ -42,7 +42,7 @@ EXP_VALU_OPS = 17
 EXP_CEILING_PER_S = FP64_PEAK_TFLOPS * 1e12 / 2 / EXP_VALU_OPS
 
 
-def gp_flops(spec, n_train, H):
+def gp_flops(spec, n_train, H, love_ranks=None):
     """Algorithmic GP flops per instance.
 
     mean+gradient: per linearisation, per stage, per evaluation, per training point:
@@ -58,7 +58,9 @@ def gp_flops(spec, n_train, H):
         evals = 4 if state_dep else 1
         per_lin += H * evals * n_train * (4 * d + 2)
         exps_lin += H * evals * n_train
-        var += H * (n_train * (n_train + 1) + 2 * n_train)
+        r = love_ranks[g] if love_ranks else None
+        # exact: triangular L^-1 k + squared norm; LOVE: R^T k (N x r) + squared norm
+        var += H * (n_train * (n_train + 1) + 2 * n_train) if r is None else H * (2 * n_train * r + 2 * r)
     return per_lin, exps_lin, var
 
 
@@ -128,6 +130,8 @@ def parse_args(argv=None):
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
+    ap.add_argument("--variance", choices=["exact", "love"], default="exact",
+                    help="tightening variance: exact, or LOVE (gpytorch fast_pred_var, rank 100) above 800 rows")
     ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
                     help="tools/pmc_summary.py output of the same command (roofline.traffic)")
     ap.add_argument("--dry-run", action="store_true",
@@ -138,7 +142,8 @@ def parse_args(argv=None):
 def workload_name(spec, args):
     N, H, B = args.n_train, args.horizon, args.batch
     return (f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}"
-            f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}, "
+            f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}"
+            f"{', LOVE variance' if getattr(args, 'variance', 'exact') == 'love' else ''}, "
             f"{B} instances per GPU, closed loop")
 
 
@@ -249,7 +254,7 @@ def run_gpu(args, rank, local_rank, world):
         me = type("Me", (), {})()
         me.gaussian_process, me.np_random = gps, np.random.default_rng(1337)
         fitc = GPMPC.precompute_sparse_posterior_mean(me, min(args.fitc, N))
-    solver.set_gps(gps, fitc=fitc)
+    solver.set_gps(gps, fitc=fitc, variance=args.variance)
     solver.set_tightening(True, 0.95, *lqr_mats)
     solver.reset(reset_iterate=True)
     traj = spec.reference_trajectory()
@@ -299,7 +304,7 @@ def run_gpu(args, rank, local_rank, world):
     qp_mean = float(sums[1]) / (total_instances * args.steps)
 
     if rank == 0:
-        per_lin, exps_lin, var_flops = gp_flops(spec, N, H)
+        per_lin, exps_lin, var_flops = gp_flops(spec, N, H, getattr(solver, "love_ranks", None))
         # dominant kernel: the SQP kernel; linearisations per instance-step = sqp_iter + 1
         sqp_ms = sqp_sum / max(len(sqp_list), 1)
         flops_sqp = B * (sqp_mean + 1.0) * per_lin          # per launch (one rank's batch)
@@ -349,7 +354,8 @@ def run_gpu(args, rank, local_rank, world):
                                  "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
                                  "Riccati recursion"},
             "roofline_variance": None if var_tf is None else {
-                "kernel": (f"gp_var_tri_kernel<{(N + 15) // 16},true>" if (N + 15) // 16 <= 16
+                "kernel": (f"gp_var_tri_kernel<{(N + 15) // 16},true>"
+                           if (N + 15) // 16 <= 16 and not any(getattr(solver, "love_ranks", None) or [])
                            else "gp_post_kernel<true>"),
                 "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},

@@ -72,6 +72,8 @@ struct gpmpc_handle {
     double* gp_linvT[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};
     double* gp_tiles[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};   // tX | tW (MFMA tile pack)
     int gp_npad[kMaxGP] = {0, 0, 0, 0};
+    double* gp_vroot[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};   // LOVE roots (tightening only)
+    int gp_vroot_cols[kMaxGP] = {0, 0, 0, 0};
     // optional per-kernel HIP-event timing (bench.py's roofline leg)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -109,6 +111,7 @@ static void free_handle(gpmpc_handle* h) {
         if (h->gp_vrows[g]) (void)hipFree(h->gp_vrows[g]);
         if (h->gp_linvT[g]) (void)hipFree(h->gp_linvT[g]);
         if (h->gp_tiles[g]) (void)hipFree(h->gp_tiles[g]);
+        if (h->gp_vroot[g]) (void)hipFree(h->gp_vroot[g]);
     }
     delete h;
 }
@@ -301,10 +304,12 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
         const double wv[4] = {alpha[i], alpha[i] * xc[0], alpha[i] * xc[1], alpha[i] * xc[2]};
         for (int j = 0; j < 4; ++j) tW[(size_t)t * 64 + (grp * 4 + j) * 4 + q] = wv[j];
     }
-    for (double** p : {&h->gp_rows[gp_id], &h->gp_vrows[gp_id], &h->gp_linvT[gp_id], &h->gp_tiles[gp_id]}) {
+    for (double** p : {&h->gp_rows[gp_id], &h->gp_vrows[gp_id], &h->gp_linvT[gp_id], &h->gp_tiles[gp_id],
+                       &h->gp_vroot[gp_id]}) {   // (a LOVE root belongs to the previous training set)
         if (*p) HIPCHK(hipFree(*p));
         *p = nullptr;
     }
+    h->gp_vroot_cols[gp_id] = 0;
     HIPCHK(hipMalloc(&h->gp_rows[gp_id], rows.size() * sizeof(double)));
     HIPCHK(hipMemcpy(h->gp_rows[gp_id], rows.data(), rows.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&h->gp_tiles[gp_id], tiles.size() * sizeof(double)));
@@ -346,6 +351,29 @@ gpmpc_status gpmpc_set_var_inputs(gpmpc_handle* h, int32_t gp_id, const int32_t*
     for (int k = 0; k < d; ++k)
         if (src[k] < 0 || src[k] >= h->md.nx + h->md.nu) return fail(GPMPC_ERR_ARG, "variance input index out of range");
     for (int k = 0; k < 3; ++k) h->md.var_src[gp_id][k] = k < d ? src[k] : 0;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_gp_variance_root(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t r, const double* R) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (gp_id < 0 || gp_id >= h->md.ngp) return fail(GPMPC_ERR_ARG, "gp_id out of range");
+    (void)hipSetDevice(h->device);
+    if (h->gp_vroot[gp_id]) {
+        (void)hipFree(h->gp_vroot[gp_id]);
+        h->gp_vroot[gp_id] = nullptr;
+        h->gp_vroot_cols[gp_id] = 0;
+    }
+    if (!R) return GPMPC_OK;   // back to the exact variance
+    if (h->gp_npad[gp_id] == 0) return fail(GPMPC_ERR_STATE, "gpmpc_set_gp first");
+    if (n != h->P.gp[gp_id].nv) return fail(GPMPC_ERR_ARG, "root rows must equal the variance GP's training rows");
+    if (r < 1 || r > 16 * 16) return fail(GPMPC_ERR_ARG, "root rank must be 1..256");
+    const int npad = h->gp_npad[gp_id], rpad = (r + 15) / 16 * 16;
+    std::vector<double> rp((size_t)npad * rpad, 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int c = 0; c < r; ++c) rp[(size_t)i * rpad + c] = R[(size_t)i * r + c];
+    HIPCHK(hipMalloc(&h->gp_vroot[gp_id], rp.size() * sizeof(double)));
+    HIPCHK(hipMemcpy(h->gp_vroot[gp_id], rp.data(), rp.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->gp_vroot_cols[gp_id] = rpad;
     return GPMPC_OK;
 }
 
@@ -489,6 +517,8 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             a.var_stride = h->md.ngp;
             a.var_off = g;
             pb.g[g] = P.gp[g];
+            pb.g[g].vroot = h->gp_vroot[g];   // LOVE (fast_pred_var) when a root is set
+            pb.g[g].vroot_cols = h->gp_vroot_cols[g];
             pb.npad[g] = h->gp_npad[g];
         }
         HIPCHK(launch_gp_post_batch(pb, true, s));

@@ -100,36 +100,41 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
         }
         return kv;
     };
-    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr);
+    const bool want_var = (a.var != nullptr) && (g.linvT != nullptr || g.vroot != nullptr);
     double sq[4] = {0.0, 0.0, 0.0, 0.0};
     if (!want_var) {
         for (int s = 0; s < npad / 4; ++s) (void)kval(4 * s + kq, true);
     } else {
-        const int ntile = npad / 16;
-        const int ct = post_ct(npad);
+        // B = (L^-1)^T (npad x npad, upper triangular: the zero triangle is skipped) or the LOVE
+        // root R (npad x vroot_cols, dense: every K row against every column)
+        const bool tri = g.vroot == nullptr;
+        const double* Bm = tri ? g.linvT : g.vroot;
+        const int ncols = tri ? npad : g.vroot_cols;
+        const int ntile = ncols / 16;
+        const int ct = post_ct(ncols);
         const int Wp = post_stride(ct);
         const int ngroups = (ntile + ct - 1) / ct;
         for (int grp = 0; grp < ngroups; ++grp) {
             const int t0 = grp * ct;
             const int tn = min(ct, ntile - t0);
-            const int npan = t0 + tn;                       // K rows < 16 (t0 + tn): upper triangle
+            const int npan = tri ? t0 + tn : npad / 16;     // K rows < 16 (t0 + tn): upper triangle
             const bool last = grp == ngroups - 1;           // the last group visits every K row
             // staged copy of panel `pan` (columns of tiles >= max(pan, t0) of this group)
             double2 stage[4];
             auto fetch = [&](int pan) {
-                const int lt0 = max(pan - t0, 0), w = 16 * (tn - lt0);
+                const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int e = 2 * (tid + j * 64 * kPostWaves);
                     const int row = e / w, col = e - row * w;
                     stage[j] = (row < 16)
-                                   ? *reinterpret_cast<const double2*>(g.linvT + (size_t)(16 * pan + row) * npad +
+                                   ? *reinterpret_cast<const double2*>(Bm + (size_t)(16 * pan + row) * ncols +
                                                                        16 * (t0 + lt0) + col)
                                    : double2{0.0, 0.0};
                 }
             };
             auto deposit = [&](int pan, double* buf) {
-                const int lt0 = max(pan - t0, 0), w = 16 * (tn - lt0);
+                const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const int e = 2 * (tid + j * 64 * kPostWaves);
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
             for (int pan = 0; pan < npan; ++pan) {
                 const double* buf = panel + (pan & 1) * 16 * Wp;
                 if (pan + 1 < npan) fetch(pan + 1);
-                const int lt0 = max(pan - t0, 0);
+                const int lt0 = tri ? max(pan - t0, 0) : 0;
                 double kvs[4];   // the panel's four kernel values first: independent exps (ILP)
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) kvs[ks] = kval(16 * pan + 4 * ks + kq, last);
@@ -309,14 +314,16 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
     size_t lds = 0;
     for (int q = 0; q < pb.n; ++q) {
         blocks = max(blocks, (pb.a[q].P + 16 * kPostWaves - 1) / (16 * kPostWaves));
-        if (pb.a[q].var != nullptr && pb.g[q].linvT != nullptr)
-            lds = std::max(lds, (size_t)2 * 16 * post_stride(post_ct(pb.npad[q])) * sizeof(double));
+        if (pb.a[q].var != nullptr && (pb.g[q].linvT != nullptr || pb.g[q].vroot != nullptr)) {
+            const int ncols = pb.g[q].vroot ? pb.g[q].vroot_cols : pb.npad[q];
+            lds = std::max(lds, (size_t)2 * 16 * post_stride(post_ct(ncols)) * sizeof(double));
+        }
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
     bool tri = true;   // every entry variance-only with the same npad <= 256
     for (int q = 0; q < pb.n; ++q)
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&
-              pb.npad[q] == pb.npad[0] && pb.npad[q] <= 16 * kMaxCT;
+              pb.g[q].vroot == nullptr && pb.npad[q] == pb.npad[0] && pb.npad[q] <= 16 * kMaxCT;
     if (tri) {
         return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, stream)
                           : launch_var_tri<false>(pb, pb.npad[0] / 16, blocks, stream);

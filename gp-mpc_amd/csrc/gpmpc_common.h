@@ -37,6 +37,11 @@ struct GPDev {
     int32_t n;
     int32_t nv;
     int32_t d;
+    // LOVE root (gpytorch fast_pred_var, gpmpc/gpmpc.py:442-444): [npad][vroot_cols] row-major,
+    // R R^T ~ (K + sn2 I)^-1; when set, the variance is sf2 - ||R^T k||^2 instead of the exact
+    // triangular form (set only in the tightening's variance launch).  NULL: exact.
+    const double* vroot;
+    int32_t vroot_cols;
     double inv_ell2;      // 1 / lengthscale^2 (isotropic RBF, gpmpc/gp.py:34)
     double sf2;           // outputscale
     double sn2;           // likelihood noise (gpmpc/gp.py:31)

@@ -32,6 +32,7 @@ SIGNATURES = {
     "gpmpc_set_options": (_I, [_P, _I, _D, _D, _D, _D, _I, _D, _D]),
     "gpmpc_set_gp": (_I, [_P, _I, _I, _I, _P, _P, _I, _P, _P, _D, _D, _D]),
     "gpmpc_use_gp": (_I, [_P, _I]),
+    "gpmpc_set_gp_variance_root": (_I, [_P, _I, _I, _I, _P]),
     "gpmpc_set_tightening": (_I, [_P, _I, _D, _P, _P, _P]),
     "gpmpc_set_var_inputs": (_I, [_P, _I, _P, _I]),
     "gpmpc_reset": (_I, [_P, _I, _I, _P]),

@@ -141,6 +141,48 @@ class GaussianProcess:
                          Linv=torch.tril(Linv))
         return self._dev
 
+    # ---------------------------------------------------------------- LOVE root
+    @torch.no_grad()
+    def love_root(self, rank: int = 100, seed: int = 0) -> torch.Tensor:
+        """Rank-r root R (n, r) with R R^T ~ (K + noise I)^-1: the predictive-covariance cache
+        gpytorch builds under ``fast_pred_var`` (LOVE), which the reference's tightening uses
+        (`gpmpc/gpmpc.py:442-444`).  Restated from gpytorch / linear_operator
+        (``root_inv_decomposition`` -> ``lanczos_tridiag``, full reorthogonalisation;
+        ``max_root_decomposition_size`` = 100 by default): Lanczos on K + noise I from a normal
+        start vector, T = V diag(lam) V^T, R = Q V diag(lam)^-1/2.  gpytorch draws the start
+        vector from torch's global generator; here it is seeded (``seed``).  gpytorch takes this
+        path only above ``max_cholesky_size`` (800 rows) and the exact Cholesky root below it
+        (see ``love_rows``)."""
+        if self.K is None:
+            self.K, self.K_inv = self.compute_covariances()
+        K = self.K
+        n = K.shape[0]
+        k = min(int(rank), n)
+        gen = torch.Generator(device="cpu").manual_seed(int(seed))
+        q = torch.randn(n, dtype=torch.float64, generator=gen).to(K.device)
+        Q = torch.zeros(n, k, dtype=torch.float64, device=K.device)
+        alpha = torch.zeros(k, dtype=torch.float64, device=K.device)
+        beta = torch.zeros(k, dtype=torch.float64, device=K.device)
+        q = q / q.norm()
+        m = k
+        for j in range(k):
+            Q[:, j] = q
+            v = K @ q
+            alpha[j] = q @ v
+            v = v - alpha[j] * q - (beta[j - 1] * Q[:, j - 1] if j > 0 else 0.0)
+            for _ in range(2):   # full reorthogonalisation (twice is enough)
+                v = v - Q[:, : j + 1] @ (Q[:, : j + 1].T @ v)
+            b = v.norm()
+            if j + 1 == k or b <= 1e-12 * alpha[: j + 1].abs().max():
+                m = j + 1
+                break
+            beta[j] = b
+            q = v / b
+        T = torch.diag(alpha[:m]) + torch.diag(beta[: m - 1], 1) + torch.diag(beta[: m - 1], -1)
+        lam, V = torch.linalg.eigh(T)
+        lam = lam.clamp_min(torch.finfo(torch.float64).tiny)
+        return (Q[:, :m] @ V) * lam.rsqrt()
+
     # ---------------------------------------------------------------- posterior on the GPU
     @torch.no_grad()
     def predict(self, z: torch.Tensor, with_noise: bool = False, return_var: bool = True):
@@ -204,3 +246,7 @@ def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: st
         p.requires_grad_(False)
     gp._dev = None
     gp.K, gp.K_inv = gp.compute_covariances()
+
+
+# gpytorch.settings.max_cholesky_size default: below it the LOVE cache is the exact Cholesky root
+LOVE_CHOLESKY_ROWS = 800

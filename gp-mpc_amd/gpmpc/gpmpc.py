@@ -35,7 +35,8 @@ class GPMPC:
     def __init__(self, symbolic_model, traj: np.ndarray | None = None, prior_params: dict | None = None,
                  horizon: int = 25, q_mpc: list | None = None, r_mpc: list | None = None, sparse_gp: bool = False,
                  prob: float = 0.955, max_gp_samples: int = 30, seed: int = 1337, device: str = "cuda",
-                 output_dir: Path | None = None, batch: int = 1, variance_inputs: str = "reference", **solver_kw):
+                 output_dir: Path | None = None, batch: int = 1, variance_inputs: str = "reference",
+                 variance: str = "exact", **solver_kw):
         spec = (symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)).copy()
         # "reference": the variance input map of `gpmpc/gpmpc.py:437-444` (for quad3d it indexes the
         # full state-input vector with the GP-input-space indices); "dynamics": each GP's own inputs
@@ -44,6 +45,9 @@ class GPMPC:
         elif variance_inputs != "reference":
             raise ValueError("variance_inputs must be 'reference' or 'dynamics'")
         self.model = spec
+        # tightening variance: "exact" (L^-1 k), or "love": gpytorch fast_pred_var's Lanczos root
+        # above 800 training rows, as the reference's propagate_constraint_limits (gpmpc.py:442-444)
+        self.variance = variance
         if q_mpc is not None:
             spec.q_diag = np.asarray(q_mpc, dtype=np.float64)
         if r_mpc is not None:
@@ -203,7 +207,7 @@ class GPMPC:
             if self.sparse:
                 n = self.gaussian_process[0].train_targets.shape[0]
                 fitc = self.precompute_sparse_posterior_mean(min(n, self.max_gp_samples))
-            self.solver.set_gps(self.gaussian_process, with_variance=True, fitc=fitc)
+            self.solver.set_gps(self.gaussian_process, with_variance=True, fitc=fitc, variance=self.variance)
             self._requires_recompile = False
             # new GPs: the reference builds a fresh AcadosOcpSolver (`gpmpc/gpmpc.py:97-108`), whose
             # memory -- iterate and multipliers -- starts from zero

@@ -16,7 +16,7 @@ import scipy.stats
 import torch
 
 from . import _lib
-from .gp import GaussianProcess
+from .gp import LOVE_CHOLESKY_ROWS, GaussianProcess
 from .models import ModelSpec
 
 STATUS_NAMES = {0: "SUCCESS", 1: "NAN_DETECTED", 2: "MAXITER", 3: "MINSTEP", 4: "QP_FAILURE"}
@@ -108,9 +108,19 @@ class BatchSolver:
         self.traj = traj
         _lib.check(self.lib.gpmpc_set_reference(self._h, traj.ctypes.data, traj.shape[1]))
 
-    def set_gps(self, gps: list[GaussianProcess] | None, with_variance: bool = True, fitc: list | None = None):
+    def set_gps(self, gps: list[GaussianProcess] | None, with_variance: bool = True, fitc: list | None = None,
+                variance: str = "exact", love_rank: int = 100, love_force: bool = False):
         """Upload GP replicas.  ``fitc[g] = (S (M,d), w (M,))`` replaces GP g's mean by the FITC
-        approximation (the variance stays exact, as in `gpmpc/gpmpc.py:441-445`)."""
+        approximation (the variance stays exact, as in `gpmpc/gpmpc.py:441-445`).
+
+        ``variance="love"``: the tightening variance of GPs with more than
+        ``LOVE_CHOLESKY_ROWS`` (800) training rows uses the rank-``love_rank`` Lanczos root
+        (`GaussianProcess.love_root`), as gpytorch's ``fast_pred_var`` does in the reference
+        (`gpmpc/gpmpc.py:442-444`); smaller GPs keep the exact root, like gpytorch's Cholesky
+        path.  ``love_force`` applies the Lanczos root at every size (tests)."""
+        if variance not in ("exact", "love"):
+            raise ValueError("variance must be 'exact' or 'love'")
+        self.love_ranks = [None] * self.spec.n_gp   # columns of each GP's LOVE root (None: exact)
         if gps is None:
             _lib.check(self.lib.gpmpc_use_gp(self._h, 0))
             self.gps = None
@@ -131,6 +141,10 @@ class BatchSolver:
                 _lib.check(self.lib.gpmpc_set_gp(self._h, g, X.shape[0], X.shape[1], X.ctypes.data, alpha.ctypes.data,
                                                  0, None, None if Linv is None else Linv.ctypes.data,
                                                  gp.lengthscale, gp.outputscale, gp.noise))
+            if with_variance and variance == "love" and (love_force or X.shape[0] > LOVE_CHOLESKY_ROWS):
+                R = _c(gp.love_root(love_rank).cpu().numpy())
+                _lib.check(self.lib.gpmpc_set_gp_variance_root(self._h, g, R.shape[0], R.shape[1], R.ctypes.data))
+                self.love_ranks[g] = R.shape[1]
         _lib.check(self.lib.gpmpc_use_gp(self._h, 1))
         self.gps = gps
 

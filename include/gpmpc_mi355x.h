@@ -84,6 +84,14 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
                           const double* alpha, int32_t nv, const double* Xv, const double* Linv,
                           double lengthscale, double outputscale, double noise);
 
+/* LOVE variance for the constraint tightening (replaces GaussianProcess predictive variance
+ * under gpytorch.settings.fast_pred_var, gpmpc/gpmpc.py:442-444): R [n][r] row-major with
+ * R R^T ~ (K(Xv,Xv) + noise I)^-1 (a rank-r Lanczos root, gpmpc/gp.py love_root); the tightening
+ * variance becomes outputscale - ||R^T k(z, Xv)||^2 + noise.  n must equal the GP's nv,
+ * 1 <= r <= 256.  R = NULL restores the exact variance; gpmpc_set_gp clears the root.
+ * gpmpc_gp_predict / gpmpc_gp_posterior stay exact. */
+gpmpc_status gpmpc_set_gp_variance_root(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t r, const double* R);
+
 /* Enable (1) / disable (0) the GP residual in the dynamics: 0 = nominal MPC
  * (gpmpc/mpc.py, prior dynamics only). */
 gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled);

@@ -92,11 +92,17 @@ def test_gp_predict_edge_cases():
     assert abs(float(m[0])) < 1e-12 and abs(float(v[0]) - hyp[1][1]) < 1e-12
 
 
-@pytest.mark.parametrize("name,N,H,B,steps,M", [("quad2d", 200, 30, 4, 3, None), ("cartpole", 50, 20, 3, 3, None),
-                                                 ("quad3d", 60, 15, 2, 2, None), ("quad3d", 120, 40, 1, 2, 60),
-                                                 ("quad2d", 1000, 30, 2, 2, None)])
-def test_closed_loop_parity(name, N, H, B, steps, M):
-    """M: FITC mean on M inducing rows (`gpmpc/gpmpc.py:377-400`, config 5's sparse GP), exact variance."""
+@pytest.mark.parametrize("name,N,H,B,steps,M,love", [("quad2d", 200, 30, 4, 3, None, False),
+                                                      ("cartpole", 50, 20, 3, 3, None, False),
+                                                      ("quad3d", 60, 15, 2, 2, None, False),
+                                                      ("quad3d", 120, 40, 1, 2, 60, False),
+                                                      ("quad2d", 1000, 30, 2, 2, None, False),
+                                                      ("quad2d", 200, 30, 3, 3, None, True),
+                                                      ("quad3d", 120, 40, 1, 2, 60, True)])
+def test_closed_loop_parity(name, N, H, B, steps, M, love):
+    """M: FITC mean on M inducing rows (`gpmpc/gpmpc.py:377-400`, config 5's sparse GP), exact variance.
+    love: the tightening variance from the LOVE root (gpytorch fast_pred_var, `gpmpc/gpmpc.py:442-444`;
+    forced at every size here), the oracle's variance from the same root (oracle.love_var)."""
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
@@ -106,10 +112,14 @@ def test_closed_loop_parity(name, N, H, B, steps, M):
     fitc = fitc_weights(gpp, M) if M else None
     if fitc is not None:
         gpo = fitc_oracle_gps(gpo, fitc)
+    if love:
+        for og, gp in zip(gpo, gpp):
+            R = gp.love_root(100).cpu().numpy()
+            og.var = (lambda Z, with_noise=True, og=og, R=R: O.love_var(og, R, Z, with_noise))
     mats = lqr(spec)
     tol = 1e-9
     solver = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)  # tight KKT for parity
-    solver.set_gps(gpp, fitc=fitc)
+    solver.set_gps(gpp, fitc=fitc, variance="love" if love else "exact", love_force=love)
     solver.set_tightening(True, 0.95, *mats)
     solver.reset(reset_iterate=True)
     sd = spec.to_dict()
