@@ -328,6 +328,7 @@ struct SqpKernel {
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
         double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
+        double *Dp, *Eb, *XT, *RV;   // cyclic-reduction solver (kCR)
         int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
@@ -351,6 +352,15 @@ struct SqpKernel {
                               + (size_t)H * NU * NU          // Ru_k^-1
                               + (size_t)(H + 1) * NB * 2     // hq, gq
                               + (size_t)(H + 1) * NX;        // dx (forward sweep)
+        if (kCR) {
+            // no Riccati stores (K', Ru^-1, dx, P', A'): the cyclic-reduction region, aliased by the GP
+            // evaluation scratch (linearisation) and the tightening scratch
+            const size_t base = (size_t)64 + 8 + 8 + (size_t)H * NX * GS + (size_t)(H + 1) * NB * 2;
+            size_t reg = cr_region(H);
+            if (gp_scratch(H) > reg) reg = gp_scratch(H);
+            if (tight_scratch(H) > reg) reg = tight_scratch(H);
+            return base + reg;
+        }
         if (kMfma) {
             const size_t acl = (size_t)H * NX * PS;            // closed-loop A'_k (tightening scratch aliases it)
             return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H));
@@ -365,6 +375,23 @@ struct SqpKernel {
         L.zero = s;  s += 8;
         L.ctrl = reinterpret_cast<int*>(s);  s += 8;
         L.G = s;   s += (size_t)H * NX * GS;
+        if constexpr (kCR) {
+            L.hq = s;  s += (size_t)(H + 1) * NB;
+            L.gq = s;  s += (size_t)(H + 1) * NB;
+            L.gz = s;
+            L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
+            L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
+            L.gsh = L.gs + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
+            L.cd = s;
+            L.Sig = s + (size_t)H * NUNC;
+            L.Dp = s;  s += (size_t)H * TT;
+            L.Eb = s;  s += cr_eb_blocks(H) * TB;
+            L.XT = s;
+            const size_t xt = (size_t)2 * (H / 2) * TB, tv = (size_t)H * NX;
+            s += xt > tv ? xt : tv;
+            L.RV = s;
+            return L;
+        }
         L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
         L.hq = s;  s += (size_t)(H + 1) * NB;
@@ -1606,6 +1633,72 @@ struct SqpKernel {
         }
     }
 
+    // ---------------------------------------------------------------- DPP-free 4-block sweeps
+    // y_{k+1} = M_k y_k over the homogeneous 8-vector with no VALU on the recursion: the state is
+    // kept twice, yA (slots 0,1: y_lo, slots 2,3: y_hi) and yB (halves swapped), and a stage is four
+    // v_mfma_f64_4x4x4_4b, two accumulation chains of two:
+    //   A: slot half h computes y'_h = M_{h,h} y_h   (B = yA in place) + M_{h,1-h} y_{1-h}   (B = yB)
+    //   B: slot half h computes y'_{1-h} = M_{1-h,1-h} y_{1-h} (B = yB) + M_{1-h,h} y_h     (B = yA)
+    // so both outputs land exactly in the B layout of the next stage (result -> B operand and
+    // accumulator chains only).  Lane (r, b, c) supplies A_b[m = c][k = r] = M[4I + c][4J + r].
+    // `mget(k, row, col)` streams: a per-lane (pointer, stride) for each of the four blocks.
+    struct Sweep4 {
+        const double* p[4];
+        int st[4];
+    };
+    // blocks (I, J) of instructions 1A, 2A, 1B, 2B for slot half h
+    __device__ static void sweep4_blocks(int h, int (&I)[4], int (&J)[4]) {
+        I[0] = h;     J[0] = h;
+        I[1] = h;     J[1] = 1 - h;
+        I[2] = 1 - h; J[2] = 1 - h;
+        I[3] = 1 - h; J[3] = h;
+    }
+    template <int DIR>
+    __device__ static void sweep4_run(Sweep4& sw, int H, double yA, double yB, double* out, int ost) {
+        double an[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) an[q] = *sw.p[q];
+        for (int k = 0; k < H; ++k) {
+            double a[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                a[q] = an[q];
+                sw.p[q] += (k + 1 < H) ? DIR * sw.st[q] : 0;
+                an[q] = *sw.p[q];
+            }
+            const double t1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a[0], yA, 0.0, 0, 0, 0);
+            const double t2 = __builtin_amdgcn_mfma_f64_4x4x4f64(a[2], yB, 0.0, 0, 0, 0);
+            const double nA = __builtin_amdgcn_mfma_f64_4x4x4f64(a[1], yB, t1, 0, 0, 0);
+            const double nB = __builtin_amdgcn_mfma_f64_4x4x4f64(a[3], yA, t2, 0, 0, 0);
+            yA = nA;
+            yB = nB;
+            *out = yA;
+            out += DIR * ost;
+        }
+    }
+
+    // Forward sweep dx_{k+1} = A'_k [dx_k; 1] (M_k = [A'_k; e_NX]) on the DPP-free scheme.
+    __device__ static void mfma4_forward2(const Lds& L, int H, int lane) {
+        static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
+        const int r = lane >> 4, c = lane & 3, b = (lane >> 2) & 3, h = b >> 1;
+        int I[4], J[4];
+        sweep4_blocks(h, I, J);
+        Sweep4 sw;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 4 * I[q] + c, col = 4 * J[q] + r;
+            const bool ld = row < NX && col <= NX;
+            sw.p[q] = ld ? L.Acl + row * PS + col : L.zero + ((row == NX && col == NX) ? 7 : 0);
+            sw.st[q] = ld ? NX * PS : 0;
+        }
+        // y_0 = [0; 1; 0]: half h's entry r (index 4h + r)
+        const double yA = (4 * h + r == NX) ? 1.0 : 0.0, yB = (4 * (1 - h) + r == NX) ? 1.0 : 0.0;
+        const bool st = c == 0 && (b == 0 || b == 2) && 4 * h + r < NX;   // yA: slot 0 lo, slot 2 hi
+        double* out = st ? L.dxv + NX + 4 * h + r : L.dummy + lane;
+        if (lane < NX) L.dxv[lane] = 0.0;
+        sweep4_run<1>(sw, H, yA, yB, out, st ? NX : 0);
+    }
+
     // Forward sweep on the VALU: dx_{k+1} = A'_k [dx_k; 1], lane i < NX owns dx[i] and the state
     // is broadcast with v_readlane (scalar operands), so the chain has no MFMA output->operand
     // latency and no LDS round trip; the rows of A'_{k+1} are fetched one stage ahead.
@@ -1648,7 +1741,7 @@ struct SqpKernel {
     // with [q; r] = gq.  Only the p recurrence is sequential (6-term VALU dot products with
     // readlane broadcast); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
-    template <bool kMfma4 = false>
+    template <int kMfma4 = 0>
     __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
@@ -1691,7 +1784,29 @@ struct SqpKernel {
             if (has1) VT[e1] = a1;
         }
         WSYNC();
-        if constexpr (kMfma4) {
+        if constexpr (kMfma4 == 2) {
+            // p_k = vt_k + A'_k^T p_{k+1} on the DPP-free 4-block scheme (sweep4_run), stages H-1 .. 0:
+            // M_k = [[A'_k[:, :NX]^T, vt_k], [0, 1]], lane (r, b, c) supplies M[4I + c][4J + r]
+            const int r = lane >> 4, c = lane & 3, b = (lane >> 2) & 3, h = b >> 1;
+            int I[4], J[4];
+            sweep4_blocks(h, I, J);
+            Sweep4 sw;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 4 * I[q] + c, col = 4 * J[q] + r;
+                const bool lda = row < NX && col < NX, ldv = row < NX && col == NX;
+                sw.p[q] = lda ? L.Acl + (size_t)(H - 1) * NX * PS + col * PS + row
+                              : (ldv ? VT + (size_t)(H - 1) * NX + row
+                                     : L.zero + ((row == NX && col == NX) ? 7 : 0));
+                sw.st[q] = lda ? NX * PS : (ldv ? NX : 0);
+            }
+            if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
+            auto yv = [&](int idx) { return idx < NX ? L.gq[H * NB + idx] : (idx == NX ? 1.0 : 0.0); };
+            const double yA = yv(4 * h + r), yB = yv(4 * (1 - h) + r);
+            const bool st = c == 0 && (b == 0 || b == 2) && 4 * h + r < NX;
+            double* out = st ? L.P + (size_t)(H - 1) * PP + PO + 4 * h + r : L.dummy + lane;
+            sweep4_run<-1>(sw, H, yA, yB, out, st ? PP : 0);
+        } else if constexpr (kMfma4 == 1) {
             // p_k = vt_k + A'_k^T p_{k+1} as the homogeneous recurrence [p_k; 1] = M_k [p_{k+1}; 1],
             // M_k = [[A'_k[:, :NX]^T, vt_k], [0, 1]] (mfma4_stage), stages H-1 .. 0
             const Mfma4Lane q = mfma4_lane(lane);
@@ -1909,6 +2024,328 @@ struct SqpKernel {
             const double lo = ddf[j < NB ? j : 0];
             const double up = (NV + j < NB) ? ddf[NV + j < NB ? NV + j : 0] : 0.0;
             dd[j] = vb ? up : lo;
+        }
+    }
+
+    // ------------------------------------------------------------------ Newton systems by cyclic reduction
+    // The IPM's Newton system  diag(h) dd + C' dp = -g,  C dd = c  (rows of C: dx_{k+1} - A_k dx_k -
+    // B_k du_k; c_k is column NB of G'_k) has a diagonal Hessian h (LINEAR_LS weights + barrier), so dd
+    // eliminates variable by variable and the dynamics multipliers pi = -dp solve the dual Schur
+    // complement, a block-tridiagonal SPD system of H blocks of NX:
+    //   Y_kk = G_k diag(ih_k) G_k' + diag(ihx_{k+1}),   Y_{k+1,k} = E_k = -A_{k+1} diag(ihx_{k+1}),
+    //   Y pi = rhs,  rhs_k = c_k + zx_{k+1} - G_k z_k,   ih = 1/h, z = ih g   (G_k = [A_k B_k];
+    //   ih = 0 for the fixed x_0 and the absent u_H),   dd = ih (C' pi - g).
+    // Odd-even cyclic reduction solves it in ceil(log2 H) levels, each parallel over its blocks
+    // (one lane per block or per block column), instead of H sequential Riccati stages: level l
+    // eliminates its odd blocks m with Cholesky factors L_m and X^l_m = L_m^-1 E_{m-1},
+    // X^r_m = L_m^-1 E_m' (one triangular solve per column), and updates the even ones,
+    //   D'_m = D_m - X^r_{m-1}' X^r_{m-1} - X^l_{m+1}' X^l_{m+1},   E'_m = -X^r_{m+1}' X^l_{m+1}.
+    // Storage: D (packed lower, Cholesky factors in place, 1/L_ii on the diagonal), the couplings of
+    // the levels >= 1 (level 0's come from G' and ih on the fly), the X blocks of the current level
+    // (they share their space with the solve's temporary vector) and the right-hand side, which the
+    // solve overwrites with pi.  (tools/cr_proto.py: same IPM iteration counts as the dense KKT.)
+    // Measured (tools/ab_variants.sh, quad2d H=30, B=1024): correct (every GPU parity test passes
+    // with it) but slower than the MFMA Riccati recursion -- SQP kernel 0.69 vs 0.38 ms: one wave
+    // issues an f64 op every ~5.5 cycles, and 6x6 blocks leave most lanes of a level idle, so the
+    // log-depth levels cost more than the 30 sequential 16x16x4 MFMA stages.  Opt-in: -DGPMPC_CR.
+#ifdef GPMPC_CR
+    static constexpr bool kCR = kMfma;
+#else
+    static constexpr bool kCR = false;
+#endif
+    static constexpr int TT = NX * (NX + 1) / 2, TB = NX * NX;
+    __host__ __device__ static constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
+    // blocks n and coupling offset eo (in blocks, levels >= 1) of level l; uniform scalar arithmetic
+    // (no per-level arrays: a runtime-indexed private array would live in scratch memory)
+    __host__ __device__ static void cr_level(int H, int l, int& n, int& eo) {
+        n = H;
+        eo = 0;
+        for (int q = 0; q < l; ++q) {
+            if (q >= 1) eo += n - 1;
+            n -= n >> 1;
+        }
+    }
+    __host__ __device__ static int cr_nlev(int H) {
+        int l = 0;
+        for (int n = H; n > 1; n -= n >> 1) ++l;
+        return l;
+    }
+    __host__ __device__ static size_t cr_eb_blocks(int H) {
+        size_t s = 0;
+        int n = H;
+        while (n > 1) {
+            n -= n >> 1;
+            s += (size_t)(n - 1);
+        }
+        return s;
+    }
+    __host__ __device__ static size_t cr_region(int H) {
+        const size_t xt = (size_t)2 * (H / 2) * TB, tv = (size_t)H * NX;
+        return (size_t)H * TT + cr_eb_blocks(H) * TB + (xt > tv ? xt : tv) + (size_t)H * NX;
+    }
+
+    // coupling E_m = Y_{m+1,m} of level l, entry (r, c)
+    __device__ static double cr_e(const Lds& L, int l, int eo, int m, int r, int c) {
+        if (l == 0) return -L.G[(size_t)(m + 1) * NX * GS + r * GS + c] * L.hq[(m + 1) * NB + c];
+        return L.Eb[(size_t)(eo + m) * TB + c * NX + r];
+    }
+    // b <- L^-1 b (packed lower factor, reciprocal diagonal)
+    __device__ static void cr_lsolve(const double* f, double (&b)[NX]) {
+        double a[TT];
+#pragma unroll
+        for (int q = 0; q < TT; ++q) a[q] = f[q];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) {
+            double acc = b[r];
+#pragma unroll
+            for (int k = 0; k < r; ++k) acc = fma(-a[tri(r, k)], b[k], acc);
+            b[r] = acc * a[tri(r, r)];
+        }
+    }
+    // b <- D^-1 b = L^-T L^-1 b
+    __device__ static void cr_dsolve(const double* f, double (&b)[NX]) {
+        double a[TT];
+#pragma unroll
+        for (int q = 0; q < TT; ++q) a[q] = f[q];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) {
+            double acc = b[r];
+#pragma unroll
+            for (int k = 0; k < r; ++k) acc = fma(-a[tri(r, k)], b[k], acc);
+            b[r] = acc * a[tri(r, r)];
+        }
+#pragma unroll
+        for (int r = NX - 1; r >= 0; --r) {
+            double acc = b[r];
+#pragma unroll
+            for (int k = r + 1; k < NX; ++k) acc = fma(-a[tri(k, r)], b[k], acc);
+            b[r] = acc * a[tri(r, r)];
+        }
+    }
+    // in-place Cholesky of a packed SPD block: L (lower), 1/L_ii on the diagonal
+    __device__ static bool cr_chol(double* f) {
+        double a[TT];
+#pragma unroll
+        for (int q = 0; q < TT; ++q) a[q] = f[q];
+        bool ok = true;
+#pragma unroll
+        for (int c = 0; c < NX; ++c) {
+            double d = a[tri(c, c)];
+#pragma unroll
+            for (int k = 0; k < c; ++k) d = fma(-a[tri(c, k)], a[tri(c, k)], d);
+            ok = ok && (d > 0.0);
+            const double is = fast_rcp(__builtin_sqrt(d));
+            a[tri(c, c)] = is;
+#pragma unroll
+            for (int r = c + 1; r < NX; ++r) {
+                double v = a[tri(r, c)];
+#pragma unroll
+                for (int k = 0; k < c; ++k) v = fma(-a[tri(r, k)], a[tri(c, k)], v);
+                a[tri(r, c)] = v * is;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < TT; ++q) f[q] = a[q];
+        return ok;
+    }
+
+    // Y's diagonal blocks (packed lower), one lane per block column
+    __device__ static void cr_build(const Lds& L, int H, int lane) {
+        for (int t = lane; t < H * NX; t += 64) {
+            const int k = t / NX, c = t - k * NX;
+            const double* Gk = L.G + (size_t)k * NX * GS;
+            const double* ih = L.hq + k * NB;
+            double wv[NB];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) wv[v] = Gk[c * GS + v] * ih[v];
+            const double dn = L.hq[(k + 1) * NB + c];
+            double* D = L.Dp + (size_t)k * TT;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                if (r < c) continue;
+                double acc = (r == c) ? dn : 0.0;
+#pragma unroll
+                for (int v = 0; v < NB; ++v) acc = fma(Gk[r * GS + v], wv[v], acc);
+                D[tri(r, c)] = acc;
+            }
+        }
+    }
+
+    __device__ static bool cr_factor(const Lds& L, int H, int lane) {
+        bool ok = true;
+        int n = H, eo = 0, eon = 0;   // level l: blocks, coupling offsets of levels l and l + 1
+        for (int l = 0; n > 1; ++l) {
+            const int ne = n >> 1, ns = n - ne;
+            // F1: Cholesky of the odd blocks
+            for (int e = lane; e < ne; e += 64) ok = cr_chol(L.Dp + (size_t)((2 * e + 1) << l) * TT) && ok;
+            WSYNC();
+            // F2: X^l_m (columns q < NX) and X^r_m (q >= NX) of the odd blocks m = 2e + 1
+            for (int t = lane; t < ne * 2 * NX; t += 64) {
+                const int e = t / (2 * NX), q = t - e * 2 * NX, m = 2 * e + 1;
+                const bool right = q >= NX;
+                const int c = right ? q - NX : q;
+                if (right && m + 1 >= n) continue;
+                double bv[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) bv[r] = right ? cr_e(L, l, eo, m, c, r) : cr_e(L, l, eo, m - 1, r, c);
+                cr_lsolve(L.Dp + (size_t)(m << l) * TT, bv);
+                double* X = L.XT + (size_t)(2 * e + (right ? 1 : 0)) * TB + c * NX;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) X[r] = bv[r];
+            }
+            WSYNC();
+            // F3: D' of the even blocks (one lane per column) and the couplings of level l + 1
+            for (int t = lane; t < ns * NX; t += 64) {
+                const int s = t / NX, c = t - s * NX, m = 2 * s;
+                const bool hl = s >= 1, hr = m + 1 < n;
+                const double* Xa = L.XT + (size_t)(2 * (hl ? s - 1 : 0) + 1) * TB;   // X^r_{m-1}
+                const double* Xb = L.XT + (size_t)(2 * (hr ? s : 0)) * TB;            // X^l_{m+1}
+                double xa[NX], xb[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) {
+                    xa[j] = hl ? Xa[c * NX + j] : 0.0;
+                    xb[j] = hr ? Xb[c * NX + j] : 0.0;
+                }
+                double* D = L.Dp + (size_t)(m << l) * TT;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    if (r < c) continue;
+                    double acc = D[tri(r, c)];
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) acc = fma(-(hl ? Xa[r * NX + j] : 0.0), xa[j], acc);
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) acc = fma(-(hr ? Xb[r * NX + j] : 0.0), xb[j], acc);
+                    D[tri(r, c)] = acc;
+                }
+            }
+            const int nc = ns - 1;   // couplings of level l + 1
+            for (int t = lane; t < nc * NX; t += 64) {
+                const int s = t / NX, c = t - s * NX;
+                const double* Xr = L.XT + (size_t)(2 * s + 1) * TB;
+                const double* Xl = L.XT + (size_t)(2 * s) * TB;
+                double xl[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) xl[j] = Xl[c * NX + j];
+                double* Eo = L.Eb + (size_t)(eon + s) * TB + c * NX;
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    double acc = 0.0;
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) acc = fma(-Xr[r * NX + j], xl[j], acc);
+                    Eo[r] = acc;
+                }
+            }
+            WSYNC();
+            eo = eon;
+            eon += nc;
+            n = ns;
+        }
+        if (lane == 0) ok = cr_chol(L.Dp) && ok;   // the last block (original index 0)
+        WSYNC();
+        return wave_max(ok ? 0.0 : 1.0) == 0.0;
+    }
+
+    // right-hand side rhs_k = c_k + zx_{k+1} - G_k z_k of the current gq
+    __device__ static void cr_rhs(const Lds& L, int H, int lane) {
+        for (int t = lane; t < H * NX; t += 64) {
+            const int k = t / NX, i = t - k * NX;
+            const double* Gr = L.G + (size_t)k * NX * GS + i * GS;
+            double acc = fma(L.gq[(k + 1) * NB + i], L.hq[(k + 1) * NB + i], Gr[NB]);
+#pragma unroll
+            for (int v = 0; v < NB; ++v) acc = fma(-Gr[v], L.gq[k * NB + v] * L.hq[k * NB + v], acc);
+            L.RV[t] = acc;
+        }
+    }
+
+    // Y pi = rhs (in RV), pi overwrites RV
+    __device__ static void cr_solve(const Lds& L, int H, int lane) {
+        double* RV = L.RV;
+        double* TV = L.XT;
+        const int nlev = cr_nlev(H);
+        for (int l = 0; l < nlev; ++l) {
+            int n, eo;
+            cr_level(H, l, n, eo);
+            const int ne = n >> 1, ns = n - ne;
+            for (int e = lane; e < ne; e += 64) {   // t_m = D_m^-1 r_m
+                const int o = (2 * e + 1) << l;
+                double bv[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) bv[r] = RV[o * NX + r];
+                cr_dsolve(L.Dp + (size_t)o * TT, bv);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) TV[o * NX + r] = bv[r];
+            }
+            WSYNC();
+            for (int t = lane; t < ns * NX; t += 64) {   // r_m -= E_{m-1} t_{m-1} + E_m' t_{m+1}
+                const int s = t / NX, r = t - s * NX, m = 2 * s;
+                double acc = RV[(m << l) * NX + r];
+                if (s >= 1) {
+                    const double* tm = TV + ((m - 1) << l) * NX;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m - 1, r, c), tm[c], acc);
+                }
+                if (m + 1 < n) {
+                    const double* tp = TV + ((m + 1) << l) * NX;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m, c, r), tp[c], acc);
+                }
+                RV[(m << l) * NX + r] = acc;
+            }
+            WSYNC();
+        }
+        if (lane == 0) {
+            double bv[NX];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) bv[r] = RV[r];
+            cr_dsolve(L.Dp, bv);
+#pragma unroll
+            for (int r = 0; r < NX; ++r) RV[r] = bv[r];
+        }
+        WSYNC();
+        for (int l = nlev - 1; l >= 0; --l) {
+            int n, eo;
+            cr_level(H, l, n, eo);
+            const int ne = n >> 1;
+            for (int t = lane; t < ne * NX; t += 64) {   // v_m = r_m - E_{m-1} pi_{m-1} - E_m' pi_{m+1}
+                const int e = t / NX, r = t - e * NX, m = 2 * e + 1;
+                double acc = RV[(m << l) * NX + r];
+                const double* pm = RV + ((m - 1) << l) * NX;
+#pragma unroll
+                for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m - 1, r, c), pm[c], acc);
+                if (m + 1 < n) {
+                    const double* pp = RV + ((m + 1) << l) * NX;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m, c, r), pp[c], acc);
+                }
+                TV[(m << l) * NX + r] = acc;
+            }
+            WSYNC();
+            for (int e = lane; e < ne; e += 64) {   // pi_m = D_m^-1 v_m
+                const int o = (2 * e + 1) << l;
+                double bv[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) bv[r] = TV[o * NX + r];
+                cr_dsolve(L.Dp + (size_t)o * TT, bv);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) RV[o * NX + r] = bv[r];
+            }
+            WSYNC();
+        }
+    }
+
+    // dp_kq = -pi_kq and this lane's step dd = ih (C' pi - g) = -ih (g + C' dp)
+    template <bool SPL, int NV>
+    __device__ static void recover_cr(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dp[i] = (kq < H) ? -L.RV[min(kq, H - 1) * NX + i] : 0.0;
+        double ctq[NV];
+        ctpi_q<SPL, NV>(L, H, kq, vb, dp, ctq);
+        const int kk = min(kq, H);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int v = vb + j;
+            const bool av = v < NX ? (kq >= 1 && kq <= H) : (v < NB && kq < H);
+            dd[j] = av ? -(L.gq[kk * NB + v] + ctq[j]) * L.hq[kk * NB + v] : 0.0;
         }
     }
 
@@ -2227,7 +2664,9 @@ struct SqpKernel {
                         mu_l += av ? ll[j] * sl[j] + lu[j] * su[j] : 0.0;
                         if (on_q && vb + j < NB) {
                             // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
-                            L.hq[k_q * NB + vb + j] = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
+                            const double hv = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
+                            if constexpr (kCR) L.hq[k_q * NB + vb + j] = av ? fast_rcp(hv) : 0.0;   // ih = 1/h
+                            else L.hq[k_q * NB + vb + j] = hv;
                             L.gq[k_q * NB + vb + j] = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
                         }
                     }
@@ -2245,7 +2684,18 @@ struct SqpKernel {
                     WSYNC();
                     TPHASE(4);
                     double dd[NV], dp[NX];
-                    if constexpr (kMfma) {
+                    if constexpr (kCR) {
+                        cr_build(L, H, lane);
+                        WSYNC();
+                        if (!cr_factor(L, H, lane)) { qp_ok = false; break; }
+                        TPHASE(6);
+                        cr_rhs(L, H, lane);
+                        WSYNC();
+                        cr_solve(L, H, lane);
+                        TPHASE(9);
+                        recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
+                        TPHASE(3);
+                    } else if constexpr (kMfma) {
                         if (!mfma_backward_h(L, H, lane)) { qp_ok = false; break; }
                         WSYNC();
                         TPHASE(8);
@@ -2254,6 +2704,8 @@ struct SqpKernel {
                         TPHASE(6);
 #ifdef GPMPC_SWEEP_VALU
                         valu_forward(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                        mfma4_forward2(L, H, lane);
 #else
                         mfma4_forward(L, H, lane);
 #endif
@@ -2316,11 +2768,20 @@ struct SqpKernel {
                     }
                     WSYNC();
                     TPHASE(5);
-                    if constexpr (kMfma) {
+                    if constexpr (kCR) {
+                        cr_rhs(L, H, lane);
+                        WSYNC();
+                        cr_solve(L, H, lane);
+                        TPHASE(9);
+                        recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
+                        TPHASE(3);
+                    } else if constexpr (kMfma) {
 #ifdef GPMPC_SWEEP_VALU
-                        valu_vector_backward<false>(L, H, lane);
+                        valu_vector_backward<0>(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                        valu_vector_backward<2>(L, H, lane);
 #else
-                        valu_vector_backward<true>(L, H, lane);
+                        valu_vector_backward<1>(L, H, lane);
 #endif
                         TPHASE(8);
                         acl_phase<false>(L, H, lane);
@@ -2328,6 +2789,8 @@ struct SqpKernel {
                         TPHASE(6);
 #ifdef GPMPC_SWEEP_VALU
                         valu_forward(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                        mfma4_forward2(L, H, lane);
 #else
                         mfma4_forward(L, H, lane);
 #endif

@@ -46,12 +46,14 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
         if constexpr (V == 11) KQ::mfma_backward<false, 4>(L, H, lane);
         if constexpr (V == 12) KQ::mfma_backward_h(L, H, lane);
         if constexpr (V == 13) KQ::mfma_backward_h<1>(L, H, lane);
+        if constexpr (V == 14) KQ::mfma4_forward2(L, H, lane);
         if constexpr (V == 8) KQ::mfma4_forward<1>(L, H, lane);
-        if constexpr (V == 1) KQ::valu_vector_backward(L, H, lane);
+        if constexpr (V == 1) KQ::valu_vector_backward<0>(L, H, lane);
         if constexpr (V == 2) KQ::template acl_phase<true>(L, H, lane);
         if constexpr (V == 3) KQ::mfma4_forward(L, H, lane);
         if constexpr (V == 4) KQ::valu_forward(L, H, lane);
-        if constexpr (V == 6) KQ::valu_vector_backward<true>(L, H, lane);
+        if constexpr (V == 6) KQ::valu_vector_backward<1>(L, H, lane);
+        if constexpr (V == 15) KQ::valu_vector_backward<2>(L, H, lane);
         if constexpr (V == 5) { double v = (double)r; for (int q = 0; q < H; ++q) v = wave_sum(v) * 1e-3; L.dummy[lane] = v; }
         WSYNC();
     }
@@ -125,32 +127,58 @@ __global__ __launch_bounds__(64) void cmp(int H, double* out) {
     }
     WSYNC();
     init_stage_data(L, H, lane, 3);
-    KQ::valu_vector_backward<false>(L, H, lane);
+    KQ::valu_vector_backward<0>(L, H, lane);
     double p1[8], k1[4];
     for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; p1[q] = e < nd ? pval(e) : 0.0; }
     for (int q = 0; q < 4; ++q) { const int e = lane + 64 * q; k1[q] = e < nk ? kval(e) : 0.0; }
     WSYNC();
     init_stage_data(L, H, lane, 3);
-    KQ::valu_vector_backward<true>(L, H, lane);
+    KQ::valu_vector_backward<1>(L, H, lane);
     double errp = 0.0, magp = 0.0;
     for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) { errp = fmax(errp, fabs(pval(e) - p1[q])); magp = fmax(magp, fabs(p1[q])); } }
     for (int q = 0; q < 4; ++q) { const int e = lane + 64 * q; if (e < nk) { errp = fmax(errp, fabs(kval(e) - k1[q])); magp = fmax(magp, fabs(k1[q])); } }
+    {   // DPP-free corrector sweep against the VALU one (p1, k1)
+        WSYNC();
+        init_stage_data(L, H, lane, 3);
+        KQ::valu_vector_backward<2>(L, H, lane);
+        double e3 = 0.0;
+        for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) e3 = fmax(e3, fabs(pval(e) - p1[q])); }
+        for (int q = 0; q < 4; ++q) { const int e = lane + 64 * q; if (e < nk) e3 = fmax(e3, fabs(kval(e) - k1[q])); }
+        e3 = wave_max(e3);
+        if (lane == 0) out[8] = e3;
+        WSYNC();
+        init_stage_data(L, H, lane, 0);
+        KQ::valu_forward(L, H, lane);
+        WSYNC();
+        for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; a[q] = e < nd ? L.dxv[e] : 0.0; }
+        WSYNC();
+    }
+    {   // DPP-free forward sweep against the stored result of the VALU sweep (a[])
+        KQ::mfma4_forward2(L, H, lane);
+        WSYNC();
+        double e2 = 0.0;
+        for (int q = 0; q < 8; ++q) { const int e = lane + 64 * q; if (e < nd) e2 = fmax(e2, fabs(L.dxv[e] - a[q])); }
+        e2 = wave_max(e2);
+        if (lane == 0) out[7] = e2;
+        WSYNC();
+    }
     err = wave_max(err); mag = wave_max(mag); errp = wave_max(errp); magp = wave_max(magp);
     if (lane == 0) { out[0] = err; out[1] = mag; out[2] = errp; out[3] = magp; }
 }
 
 static void check(int H) {
     double* d;
-    (void)hipMalloc(&d, 7 * sizeof(double));
+    (void)hipMalloc(&d, 9 * sizeof(double));
     for (int variant = 0; variant < 3; ++variant) {
         const double flag = variant;
         (void)hipMemcpy(d + 6, &flag, sizeof(double), hipMemcpyHostToDevice);
         cmp<<<1, 64, KQ::lds_doubles(H) * sizeof(double)>>>(H, d);
-        double h[6];
+        double h[9];
         (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
         printf("check forward mfma4 (both) vs valu: max |diff| %.3e (max |dx| %.3e); vector backward: %.3e (max %.3e); "
                "factor %s vs MFMA Schur: %.3e (max %.3e)\n", h[0], h[1], h[2], h[3],
                variant == 2 ? "homogeneous" : (variant ? "deferred-store" : "N-form"), h[4], h[5]);
+        printf("  DPP-free forward vs VALU forward: max |diff| %.3e; DPP-free corrector vs VALU: %.3e\n", h[7], h[8]);
     }
 }
 
@@ -198,6 +226,8 @@ int main() {
     run<11>("factor, deferred st", H, B, reps, d_out, d_sink);
     run<12>("factor, homogeneous", H, B, reps, d_out, d_sink);
     run<13>("factor, homog no st", H, B, reps, d_out, d_sink);
+    run<14>("forward (4-chain)", H, B, reps, d_out, d_sink);
+    run<15>("backward (vec 4-chain)", H, B, reps, d_out, d_sink);
     check(H);
     return 0;
 }
