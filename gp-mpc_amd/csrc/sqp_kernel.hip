@@ -329,6 +329,7 @@ struct SqpKernel {
     struct Lds {
         double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
         double *Dp, *Eb, *XT, *RV;   // cyclic-reduction solver (kCR)
+        double *Dq, *xs;             // WSPL: step-vector exchange, reduction slots
         int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
@@ -367,7 +368,8 @@ struct SqpKernel {
         }
         return common + p_region(H)                             // P'_k (packed) | GP scratch
                + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
-               + tight_scratch(H);
+               + tight_scratch(H)
+               + (NWAVES > 1 ? (size_t)(H + 1) * NB + 64 : 0);  // WSPL exchange (Dq, xs)
     }
     __device__ static Lds carve(double* s, int H) {
         Lds L{};
@@ -412,7 +414,11 @@ struct SqpKernel {
             L.Ms = s;  s += (size_t)GS * GS;
             L.vs = s;  s += (size_t)2 * NB + NX;
             L.cd = s;  s += (size_t)H * NUNC;
-            L.Sig = s;
+            L.Sig = s; s += tight_scratch(H) - (size_t)H * NUNC;
+            if constexpr (NWAVES > 1) {
+                L.Dq = s;  s += (size_t)(H + 1) * NB;
+                L.xs = s;
+            }
         }
         return L;
     }
@@ -1979,6 +1985,13 @@ struct SqpKernel {
                 const double ph = (NV + j < NX) ? pim1[NV + j < NX ? NV + j : 0] : 0.0;
                 pm = vb ? ph : pm;
             }
+            if constexpr (WSPL) {   // variable vb + j, vb = w NV uniform over the wave
+#pragma unroll
+                for (int q = 1; q < NWAVES; ++q) {
+                    const int vq = q * NV + j;
+                    if (vb == q * NV) pm = (vq < NX) ? pim1[vq < NX ? vq : 0] : 0.0;
+                }
+            }
             out[j] = (v < NB) ? (((kq < H) ? -acc : 0.0) + ((v < NX && kq >= 1 && kq <= H) ? pm : 0.0)) : 0.0;
         }
     }
@@ -2022,8 +2035,16 @@ struct SqpKernel {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const double lo = ddf[j < NB ? j : 0];
-            const double up = (NV + j < NB) ? ddf[NV + j < NB ? NV + j : 0] : 0.0;
-            dd[j] = vb ? up : lo;
+            if constexpr (WSPL) {   // vb = w NV, uniform over the wave
+                double v = lo;
+#pragma unroll
+                for (int q = 1; q < NWAVES; ++q)
+                    if (vb == q * NV) v = ddf[q * NV + j < NB ? q * NV + j : 0];
+                dd[j] = v;
+            } else {
+                const double up = (NV + j < NB) ? ddf[NV + j < NB ? NV + j : 0] : 0.0;
+                dd[j] = vb ? up : lo;
+            }
         }
     }
 
@@ -2349,6 +2370,384 @@ struct SqpKernel {
         }
     }
 
+    // ------------------------------------------------------------------ the QP (HPIPM's role), Mehrotra IPM
+    // IPM layout: lane l holds stage kq's variables v = vb + j (j < NV).  SPL: the stage vectors are
+    // split over lanes kq and kq + 32 (NV = NB/2), halving the per-lane IPM state and the elementwise
+    // work.  WSPL (NWAVES > 1, quad3d): split over the instance's waves, wave w holding variables
+    // w NV .. (w + 1) NV - 1 of every stage (lane = stage, NV = NB / NWAVES): the GP helper waves, idle
+    // outside the tile passes, take their share of the elementwise work, and no lane holds more than
+    // NV variables' IPM state (the unsplit layout spilled 3.5 KB per lane to scratch at H = 40).  The
+    // full step vector for the dynamics residual, the reductions and the Riccati status cross the
+    // waves through LDS at block barriers; the Riccati recursion runs on wave 0.
+    static constexpr bool WSPL = NWAVES > 1;
+    static_assert(!WSPL || NB % NWAVES == 0, "WSPL: whole variables per wave");
+    template <bool SPL>
+    __host__ __device__ static constexpr int nv_of() { return WSPL ? NB / NWAVES : (SPL ? (NB + 1) / 2 : NB); }
+    struct Tm {   // phase-timing state (GPMPC_TIMING)
+        unsigned long long acc[kPhases];
+        unsigned long long last;
+        int cur;
+    };
+    __device__ static void XSYNC() {
+        if constexpr (WSPL) __syncthreads();
+        else wave_sync<NWAVES>();
+    }
+    // reductions over the instance (WSPL: wave reduction, one LDS exchange with a block barrier;
+    // the two slot sets alternate, so one barrier per exchange suffices)
+    __device__ static void xred2(const Lds& L, int lane, int wv, int& par, double vmax, double vsum, double& omax,
+                                 double& osum) {
+        vmax = wave_max(vmax);
+        vsum = wave_sum(vsum);
+        if constexpr (WSPL) {
+            double* sl = L.xs + par * 2 * NWAVES;
+            if (lane == 0) {
+                sl[wv] = vmax;
+                sl[NWAVES + wv] = vsum;
+            }
+            __syncthreads();
+            vmax = sl[0];
+            vsum = sl[NWAVES];
+#pragma unroll
+            for (int q = 1; q < NWAVES; ++q) {
+                vmax = fmax(vmax, sl[q]);
+                vsum += sl[NWAVES + q];
+            }
+            par ^= 1;
+        }
+        omax = vmax;
+        osum = vsum;
+    }
+    __device__ static double xmax(const Lds& L, int lane, int wv, int& par, double v) {
+        double m, s;
+        xred2(L, lane, wv, par, v, 0.0, m, s);
+        return m;
+    }
+    __device__ static double xsum(const Lds& L, int lane, int wv, int& par, double v) {
+        double m, s;
+        xred2(L, lane, wv, par, 0.0, v, m, s);
+        return s;
+    }
+    __device__ static bool xall(const Lds& L, int lane, int wv, int& par, bool ok) {
+        return xmax(L, lane, wv, par, ok ? 0.0 : 1.0) == 0.0;
+    }
+    // dynamics residual of stage kq; WSPL: the waves exchange their parts of the step vector in LDS
+    template <bool SPL, int NV>
+    __device__ static void dyn_residual_x(const Lds& L, int H, int kq, int vb, const double (&d)[NV],
+                                          const double (&c)[NX], double (&r)[NX]) {
+        if constexpr (WSPL) {
+            if (kq <= H) {
+#pragma unroll
+                for (int j = 0; j < NV; ++j) L.Dq[(size_t)kq * NB + vb + j] = d[j];
+            }
+            __syncthreads();
+            const double* dk = L.Dq + (size_t)min(kq, H) * NB;
+            const double* dn = L.Dq + (size_t)min(kq + 1, H) * NB;
+            const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS;
+            double df[NB];
+#pragma unroll
+            for (int v = 0; v < NB; ++v) df[v] = dk[v];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double acc = dn[i] - c[i];
+#pragma unroll
+                for (int j = 0; j < NB; ++j) acc = fma(-G[i * GS + j], df[j], acc);
+                r[i] = (kq < H) ? acc : 0.0;
+            }
+        } else {
+            dyn_residual_q<SPL, NV>(L, H, kq, d, c, r);
+        }
+    }
+
+    // WSPL: this wave's QP data from what wave 0 published (hq: lower bound distances, gq: upper,
+    // Dq: cost gradient, dxv: dynamics residual, xs + 4 NWAVES: dx_0), then a barrier so that no wave
+    // overwrites the buffers before every wave has read them.
+    template <int NV>
+    __device__ static void qp_setup_pub(const ProblemDev& P, const Lds& L, int H, int lane, int wv, double (&blo)[NV],
+                                        double (&bup)[NV], double (&gv)[NV], double (&hd)[NV], double (&d)[NV],
+                                        double (&cqq)[NX]) {
+        const int kk = min(lane, H), vb = wv * NV;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const int v = vb + j;
+            blo[j] = L.hq[(size_t)kk * NB + v];
+            bup[j] = L.gq[(size_t)kk * NB + v];
+            gv[j] = L.Dq[(size_t)kk * NB + v];
+            hd[j] = hdiag(P, v, lane, H);
+            d[j] = (lane == 0 && v < NX) ? L.xs[4 * NWAVES + (v < NX ? v : 0)] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) cqq[i] = L.dxv[(size_t)kk * NX + i];
+        __syncthreads();
+    }
+    // WSPL: every wave's part of the QP step into Dq; the barrier is B2 of the helper command
+    template <int NV>
+    __device__ static void qp_publish_step(const Lds& L, int H, int lane, int wv, const double (&d)[NV]) {
+        if (lane <= H) {
+#pragma unroll
+            for (int j = 0; j < NV; ++j) L.Dq[(size_t)lane * NB + wv * NV + j] = d[j];
+        }
+        __syncthreads();
+    }
+
+    // One QP of the SQP iteration: blo/bup/gv/hd/d (this lane's variables) and cqq (the stage's
+    // dynamics residual) in, the step d, the bound multipliers and piq (dynamics multipliers of
+    // stage kq) out.  Every wave of the instance calls it (WSPL) with the same control flow.
+    template <bool SPL, int NV>
+    __device__ static bool qp_ipm(const ProblemDev& P, const Lds& L, int H, int lane, int wv, const Entries& E,
+                                  const double (&blo)[NV], const double (&bup)[NV], const double (&gv)[NV],
+                                  const double (&hd)[NV], double (&d)[NV], const double (&cqq)[NX], double (&ll)[NV],
+                                  double (&lu)[NV], double (&piq)[NX], int& qit_out, Tm& tm) {
+        const bool hi_half = SPL && lane >= 32;
+        const int kq = SPL ? (lane & 31) : lane;
+        const int vb = WSPL ? wv * NV : (hi_half ? NV : 0);
+        const bool on_q = kq <= H;
+        const bool actx_q = on_q && kq >= 1;
+        const bool actu_q = kq < H;
+        const int k_q = min(kq, H);
+        auto avq = [&](int j) { const int v = vb + j; return v < NX ? actx_q : (v < NB && actu_q); };
+        const double nc = 2.0 * (double)H * (double)NB;
+#ifdef GPMPC_TIMING
+        unsigned long long(&tacc)[kPhases] = tm.acc;
+        unsigned long long& tlast = tm.last;
+        int& tcur = tm.cur;
+#else
+        (void)tm;
+#endif
+        double sl[NV], su[NV];
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const bool av = avq(j);
+            sl[j] = av ? fmax(-blo[j], 1e-2) : 1.0;
+            su[j] = av ? fmax(bup[j], 1e-2) : 1.0;
+            ll[j] = av ? P.qp_mu0 * fast_rcp(sl[j]) : 0.0;
+            lu[j] = av ? P.qp_mu0 * fast_rcp(su[j]) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) piq[i] = 0.0;
+        bool qp_ok = true;
+        int qit = 0, par = 0;
+        TPHASE(3);
+        for (qit = 0; qit < P.qp_max_iter; ++qit) {
+            double rp[NX];
+            TPHASE(10);
+            // slack reciprocals, once per IPM iteration: every later 1/s of this iteration
+            // and the ratio-test step lengths (1 / max(-ds/s)) reuse them
+            double isl[NV], isu[NV];
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                isl[j] = fast_rcp(sl[j]);
+                isu[j] = fast_rcp(su[j]);
+            }
+            {
+                double ctq[NV];
+                ctpi_q<SPL, NV>(L, H, kq, vb, piq, ctq);
+                dyn_residual_x<SPL, NV>(L, H, kq, vb, d, cqq, rp);
+                double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const bool av = avq(j);
+                    const double rd = av ? fma(hd[j], d[j], gv[j]) - ll[j] + lu[j] + ctq[j] : 0.0;
+                    const double rl = av ? d[j] - blo[j] - sl[j] : 0.0;
+                    const double ru = av ? bup[j] - d[j] - su[j] : 0.0;
+                    m_rd = fmax(m_rd, fabs(rd));
+                    m_lu = fmax(m_lu, fmax(fabs(rl), fabs(ru)));
+                    mu_l += av ? ll[j] * sl[j] + lu[j] * su[j] : 0.0;
+                    if (on_q && vb + j < NB) {
+                        // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
+                        const double hv = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
+                        if constexpr (kCR) L.hq[k_q * NB + vb + j] = av ? fast_rcp(hv) : 0.0;   // ih = 1/h
+                        else L.hq[k_q * NB + vb + j] = hv;
+                        L.gq[k_q * NB + vb + j] = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
+                // the stopping test only needs the largest of the three residual norms: one reduction
+                double mu, m_res;
+                xred2(L, lane, wv, par, fmax(m_rd, fmax(m_rb, m_lu)), mu_l, m_res, mu);
+                mu /= nc;
+                if (!(mu == mu) || !(m_res == m_res)) { qp_ok = false; break; }
+                if (m_res <= P.qp_tol && mu <= P.qp_tol) break;
+                if (actu_q && !hi_half && wv == 0) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
+                }
+                XSYNC();
+                TPHASE(4);
+                double dd[NV], dp[NX];
+                if constexpr (kCR) {
+                    cr_build(L, H, lane);
+                    WSYNC();
+                    if (!cr_factor(L, H, lane)) { qp_ok = false; break; }
+                    TPHASE(6);
+                    cr_rhs(L, H, lane);
+                    WSYNC();
+                    cr_solve(L, H, lane);
+                    TPHASE(9);
+                    recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else if constexpr (kMfma) {
+                    if (!mfma_backward_h(L, H, lane)) { qp_ok = false; break; }
+                    WSYNC();
+                    TPHASE(8);
+                    acl_phase<true>(L, H, lane);
+                    WSYNC();
+                    TPHASE(6);
+#ifdef GPMPC_SWEEP_VALU
+                    valu_forward(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                    mfma4_forward2(L, H, lane);
+#else
+                    mfma4_forward(L, H, lane);
+#endif
+                    WSYNC();
+                    TPHASE(9);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else {
+                    // the recursion on wave 0 (WSPL: the other waves wait at the status exchange)
+                    bool rok = true;
+                    if (wv == 0) {
+                        if constexpr (kMfmaBig) {
+                            rok = mfma_backward_big(L, H, lane);
+                            WSYNC();
+                        } else {
+                            rok = riccati_factor(L, H, lane, E);
+                        }
+                        TPHASE(6);
+                        if (rok) riccati_forward(L, H, lane);
+                    }
+                    if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
+                    if (!rok) { qp_ok = false; break; }
+                    TPHASE(3);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                }
+                // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
+                // alpha_max = 1 / max(1, max_i -dv_i / v_i)
+                double rmax = 1.0, mua_l = 0.0;
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    if (avq(j)) {
+                        const double rl = d[j] - blo[j] - sl[j];
+                        const double ru = bup[j] - d[j] - su[j];
+                        const double ql = (dd[j] + rl) * isl[j], qu = (-dd[j] + ru) * isu[j];
+                        rmax = fmax(rmax, fmax(fmax(-ql, -qu), fmax(1.0 + ql, 1.0 + qu)));
+                    }
+                }
+                const double a_aff = fast_rcp(xmax(L, lane, wv, par, rmax));
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    if (avq(j)) {
+                        const double rl = d[j] - blo[j] - sl[j];
+                        const double ru = bup[j] - d[j] - su[j];
+                        const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
+                        const double ql = dsl * isl[j], qu = dsu * isu[j];
+                        mua_l += ll[j] * fma(-a_aff, 1.0 + ql, 1.0) * fma(a_aff, dsl, sl[j]) +
+                                 lu[j] * fma(-a_aff, 1.0 + qu, 1.0) * fma(a_aff, dsu, su[j]);
+                    }
+                }
+                const double mu_aff = xsum(L, lane, wv, par, mua_l) / nc;
+                const double sr = mu_aff / mu;
+                const double smu = sr * sr * sr * mu;
+                // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu  ->  gq += (dll dsl - smu)/sl - (dlu dsu - smu)/su
+                double dda[NV];
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    dda[j] = dd[j];
+                    if (on_q && avq(j)) {
+                        const double rl = d[j] - blo[j] - sl[j];
+                        const double ru = bup[j] - d[j] - su[j];
+                        const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
+                        const double dll = -ll[j] * fma(dsl, isl[j], 1.0);
+                        const double dlu = -lu[j] * fma(dsu, isu[j], 1.0);
+                        L.gq[k_q * NB + vb + j] += (dll * dsl - smu) * isl[j] - (dlu * dsu - smu) * isu[j];
+                    }
+                }
+                XSYNC();
+                TPHASE(5);
+                if constexpr (kCR) {
+                    cr_rhs(L, H, lane);
+                    WSYNC();
+                    cr_solve(L, H, lane);
+                    TPHASE(9);
+                    recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else if constexpr (kMfma) {
+#ifdef GPMPC_SWEEP_VALU
+                    valu_vector_backward<0>(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                    valu_vector_backward<2>(L, H, lane);
+#else
+                    valu_vector_backward<1>(L, H, lane);
+#endif
+                    TPHASE(8);
+                    acl_phase<false>(L, H, lane);
+                    WSYNC();
+                    TPHASE(6);
+#ifdef GPMPC_SWEEP_VALU
+                    valu_forward(L, H, lane);
+#elif defined(GPMPC_SWEEP4)
+                    mfma4_forward2(L, H, lane);
+#else
+                    mfma4_forward(L, H, lane);
+#endif
+                    WSYNC();
+                    TPHASE(9);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else {
+                    if (wv == 0) {
+                        riccati_vector(L, H, lane);
+                        TPHASE(6);
+                        riccati_forward(L, H, lane);
+                    }
+                    XSYNC();
+                    TPHASE(3);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                }
+                rmax = 1.0;
+                double dsl[NV], dsu[NV], dll[NV], dlu[NV];
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    dsl[j] = dsu[j] = dll[j] = dlu[j] = 0.0;
+                    if (avq(j)) {
+                        const double rl = d[j] - blo[j] - sl[j];
+                        const double ru = bup[j] - d[j] - su[j];
+                        const double dsla = dda[j] + rl, dsua = -dda[j] + ru;
+                        const double dlla = -ll[j] * fma(dsla, isl[j], 1.0);
+                        const double dlua = -lu[j] * fma(dsua, isu[j], 1.0);
+                        const double rml = ll[j] * sl[j] + dlla * dsla - smu;
+                        const double rmu = lu[j] * su[j] + dlua * dsua - smu;
+                        dsl[j] = dd[j] + rl;
+                        dsu[j] = -dd[j] + ru;
+                        dll[j] = (-rml - ll[j] * dsl[j]) * isl[j];
+                        dlu[j] = (-rmu - lu[j] * dsu[j]) * isu[j];
+                        const double ill = fast_rcp(ll[j]), ilu = fast_rcp(lu[j]);
+                        rmax = fmax(rmax, fmax(fmax(-dsl[j] * isl[j], -dsu[j] * isu[j]),
+                                               fmax(-dll[j] * ill, -dlu[j] * ilu)));
+                    }
+                }
+                const double alpha = fmin(1.0, 0.995 * fast_rcp(xmax(L, lane, wv, par, rmax)));
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    if (avq(j)) {
+                        d[j] = fma(alpha, dd[j], d[j]);
+                        sl[j] = fma(alpha, dsl[j], sl[j]);
+                        su[j] = fma(alpha, dsu[j], su[j]);
+                        ll[j] = fma(alpha, dll[j], ll[j]);
+                        lu[j] = fma(alpha, dlu[j], lu[j]);
+                    }
+                }
+                if (actu_q) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
+                }
+            }
+        }
+        qit_out = qit;
+        return qp_ok;
+    }
+
     // cost Hessian diagonal of stage variable v on lane k (acados cost_scaling: dt on stages, 1 terminal)
     __device__ static double hdiag(const ProblemDev& P, int v, int lane, int H) {
         if (v < NX) return (lane >= 1 && lane <= H) ? ((lane < H) ? P.cost_scale : 1.0) * P.q[v] : 1.0;
@@ -2358,13 +2757,38 @@ struct SqpKernel {
     // GP helper wave w (1..NWAVES-1): waits for the main wave's tile passes (B1), runs its share
     // of the pass's tiles into its partial buffer, and meets the main wave again (B2); the main wave
     // ends the loop with command -1 at the end of the kernel (one more B1).
-    __device__ static void helper_loop(const ProblemDev& P, const Lds& L, int w, int lane) {
+    // Command -2 (WSPL): the wave takes its variables' share of the QP (qp_ipm) and publishes its
+    // part of the step at B2.
+    __device__ static void helper_loop(const ProblemDev& P, const StateDev& S, const Lds& L, int w, int lane, int b) {
         const int H = P.H;
         const int ne = (H + 15) >> 4, np = 16 * ne;
         for (;;) {
             __syncthreads();   // B1
             const int G = L.ctrl[0];
-            if (G < 0) break;
+            if (G == -1) break;
+            if constexpr (WSPL) {
+                if (G == -2) {
+                    constexpr int NV = nv_of<false>();
+                    double blo[NV], bup[NV], gv[NV], hd[NV], d[NV], ll[NV], lu[NV], piq[NX], cqq[NX];
+                    qp_setup_pub<NV>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq);
+                    Tm tm{};
+                    int qit = 0;
+                    const bool ok = qp_ipm<false, NV>(P, L, H, lane, w, decode(lane), blo, bup, gv, hd, d, cqq, ll, lu,
+                                                      piq, qit, tm);
+                    if (ok && lane <= H) {   // this wave's bound multipliers (acados memory)
+                        double* lam_q = S.lam + ((size_t)b * (H + 1) + lane) * 2 * NB;
+#pragma unroll
+                        for (int j = 0; j < NV; ++j) {
+                            const int v = w * NV + j;
+                            const bool ab = v < NX ? (lane >= 1) : (lane < H);
+                            lam_q[v] = ab ? ll[j] : 0.0;
+                            lam_q[NB + v] = ab ? lu[j] : 0.0;
+                        }
+                    }
+                    qp_publish_step<NV>(L, H, lane, w, d);   // B2
+                    continue;
+                }
+            }
             static_for<NGP>([&](auto gi) {   // static index into the kernel-argument GP array
                 constexpr int GG = decltype(gi)::value;
                 if (GG != G) return;
@@ -2387,7 +2811,7 @@ struct SqpKernel {
         const Lds L = carve(smem, H);
         if constexpr (NWAVES > 1) {
             if (threadIdx.x >= 64) {   // GP helper wave
-                helper_loop(P, L, threadIdx.x >> 6, lane);
+                helper_loop(P, S, L, threadIdx.x >> 6, lane, b);
                 return;
             }
         }
@@ -2397,19 +2821,23 @@ struct SqpKernel {
         const bool act_u = lane < H;
         const int k = min(lane, H);
         // IPM lane layout (see the QP below): stage kq, variables vb .. vb + NV - 1
-        constexpr int NV = SPL ? (NB + 1) / 2 : NB;
+        static_assert(!(WSPL && SPL), "one IPM split at a time");
+        constexpr int NV = nv_of<SPL>();
         const bool hi_half = SPL && lane >= 32;
         const int kq = SPL ? (lane & 31) : lane;
-        const int vb = hi_half ? NV : 0;
+        const int vb = hi_half ? NV : 0;   // (WSPL: wave 0 holds variables 0 .. NV - 1)
         const bool on_q = kq <= H;
         const bool actx_q = on_q && kq >= 1;
         const bool actu_q = kq < H;
         const int k_q = min(kq, H);
         auto avq = [&](int j) { const int v = vb + j; return v < NX ? actx_q : (v < NB && actu_q); };
+        Tm tm{};
 #ifdef GPMPC_TIMING
-        unsigned long long tacc[kPhases] = {};
-        unsigned long long tlast = __builtin_amdgcn_s_memtime();
-        int tcur = 7;
+        unsigned long long(&tacc)[kPhases] = tm.acc;
+        unsigned long long& tlast = tm.last;
+        int& tcur = tm.cur;
+        tlast = __builtin_amdgcn_s_memtime();
+        tcur = 7;
 #endif
         // ---------------- load instance state (acados memory: iterate + multipliers)
         // The multipliers stay in global memory (this lane's rows of S.lam / S.pi): they are read
@@ -2515,7 +2943,6 @@ struct SqpKernel {
         }
         const bool x0_ok = v0 <= P.tol_ineq;   // uniform: x0 and the bounds are the same on every lane
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
-        const double nc = 2.0 * (double)H * (double)NB;
         int status = kMaxIter, it = 0, qp_total = 0;
         double res[4] = {0, 0, 0, 0};
         if (!x0_ok) status = kQPFailure;
@@ -2589,19 +3016,37 @@ struct SqpKernel {
             }
             if (it == P.max_iter) { status = kMaxIter; break; }
 
-            // ---------------- QP in the step variables (HPIPM's role), Mehrotra IPM
-            // IPM layout: lane l holds stage kq's variables v = vb + j (j < NV); with SPL the stage
-            // vectors are split over lanes kq and kq + 32 (NV = NB/2), halving the per-lane IPM
-            // state and the elementwise work.  qv(): variable vb + j of stage kq from a stage
-            // vector held in the lane = stage layout.
+            // ---------------- QP in the step variables (HPIPM's role): qp_ipm
+            // qv(): variable vb + j of stage kq from a stage vector held in the lane = stage layout.
             auto qv = [&](const double (&full)[NB], int j) {
                 const double lo = (j < NB) ? full[j < NB ? j : 0] : 0.0;
                 if constexpr (!SPL) return lo;
                 const double up = xor32_d((NV + j < NB) ? full[NV + j < NB ? NV + j : 0] : 0.0);   // lane kq
                 return hi_half ? up : lo;
             };
-            double blo[NV], bup[NV], gv[NV], hd[NV], d[NV], sl[NV], su[NV], ll[NV], lu[NV], piq[NX], cqq[NX];
-            {
+            double blo[NV], bup[NV], gv[NV], hd[NV], d[NV], ll[NV], lu[NV], piq[NX], cqq[NX];
+            if constexpr (WSPL) {
+                // publish the stage data for the helper waves (LDS buffers free at this point:
+                // hq <- lower bound distances, gq <- upper, Dq <- cost gradient, dxv <- dynamics
+                // residual, xs + 16 <- dx_0) and wake them for the QP (command -2)
+                if (on) {
+#pragma unroll
+                    for (int v = 0; v < NB; ++v) {
+                        L.hq[(size_t)k * NB + v] = lbv(v) - w[v];
+                        L.gq[(size_t)k * NB + v] = ubv(v) - w[v];
+                        L.Dq[(size_t)k * NB + v] = g[v];
+                    }
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) L.dxv[(size_t)k * NX + i] = cq[i];
+                }
+                if (lane == 0) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) L.xs[4 * NWAVES + i] = x0[i] - w[i];
+                    L.ctrl[0] = -2;
+                }
+                __syncthreads();   // B1
+                qp_setup_pub<NV>(P, L, H, lane, 0, blo, bup, gv, hd, d, cqq);
+            } else {
                 double lbm[NB], ubm[NB], hdf[NB], d0[NB];
 #pragma unroll
                 for (int v = 0; v < NB; ++v) {
@@ -2617,233 +3062,20 @@ struct SqpKernel {
                     gv[j] = qv(g, j);
                     hd[j] = qv(hdf, j);
                     d[j] = qv(d0, j);
-                    const bool av = avq(j);
-                    sl[j] = av ? fmax(-blo[j], 1e-2) : 1.0;
-                    su[j] = av ? fmax(bup[j], 1e-2) : 1.0;
-                    ll[j] = av ? P.qp_mu0 * fast_rcp(sl[j]) : 0.0;
-                    lu[j] = av ? P.qp_mu0 * fast_rcp(su[j]) : 0.0;
                 }
-            }
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
-                piq[i] = 0.0;
-                if constexpr (SPL) {
-                    const double o = xor32_d(cq[i]);   // lane kq for the upper half
-                    cqq[i] = hi_half ? o : cq[i];
-                } else {
-                    cqq[i] = cq[i];
+                for (int i = 0; i < NX; ++i) {
+                    if constexpr (SPL) {
+                        const double o = xor32_d(cq[i]);   // lane kq for the upper half
+                        cqq[i] = hi_half ? o : cq[i];
+                    } else {
+                        cqq[i] = cq[i];
+                    }
                 }
             }
-            bool qp_ok = true;
             int qit = 0;
-            TPHASE(3);
-            for (qit = 0; qit < P.qp_max_iter; ++qit) {
-                double rp[NX];
-                TPHASE(10);
-                // slack reciprocals, once per IPM iteration: every later 1/s of this iteration
-                // and the ratio-test step lengths (1 / max(-ds/s)) reuse them
-                double isl[NV], isu[NV];
-#pragma unroll
-                for (int j = 0; j < NV; ++j) {
-                    isl[j] = fast_rcp(sl[j]);
-                    isu[j] = fast_rcp(su[j]);
-                }
-                {
-                    double ctq[NV];
-                    ctpi_q<SPL, NV>(L, H, kq, vb, piq, ctq);
-                    dyn_residual_q<SPL, NV>(L, H, kq, d, cqq, rp);
-                    double m_rd = 0.0, m_rb = 0.0, m_lu = 0.0, mu_l = 0.0;
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        const bool av = avq(j);
-                        const double rd = av ? fma(hd[j], d[j], gv[j]) - ll[j] + lu[j] + ctq[j] : 0.0;
-                        const double rl = av ? d[j] - blo[j] - sl[j] : 0.0;
-                        const double ru = av ? bup[j] - d[j] - su[j] : 0.0;
-                        m_rd = fmax(m_rd, fabs(rd));
-                        m_lu = fmax(m_lu, fmax(fabs(rl), fabs(ru)));
-                        mu_l += av ? ll[j] * sl[j] + lu[j] * su[j] : 0.0;
-                        if (on_q && vb + j < NB) {
-                            // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
-                            const double hv = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
-                            if constexpr (kCR) L.hq[k_q * NB + vb + j] = av ? fast_rcp(hv) : 0.0;   // ih = 1/h
-                            else L.hq[k_q * NB + vb + j] = hv;
-                            L.gq[k_q * NB + vb + j] = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < NX; ++i) m_rb = fmax(m_rb, fabs(rp[i]));
-                    const double mu = wave_sum(mu_l) / nc;
-                    // the stopping test only needs the largest of the three residual norms: one reduction
-                    const double m_res = wave_max(fmax(m_rd, fmax(m_rb, m_lu)));
-                    if (!(mu == mu) || !(m_res == m_res)) { qp_ok = false; break; }
-                    if (m_res <= P.qp_tol && mu <= P.qp_tol) break;
-                    if (actu_q && !hi_half) {
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
-                    }
-                    WSYNC();
-                    TPHASE(4);
-                    double dd[NV], dp[NX];
-                    if constexpr (kCR) {
-                        cr_build(L, H, lane);
-                        WSYNC();
-                        if (!cr_factor(L, H, lane)) { qp_ok = false; break; }
-                        TPHASE(6);
-                        cr_rhs(L, H, lane);
-                        WSYNC();
-                        cr_solve(L, H, lane);
-                        TPHASE(9);
-                        recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
-                        TPHASE(3);
-                    } else if constexpr (kMfma) {
-                        if (!mfma_backward_h(L, H, lane)) { qp_ok = false; break; }
-                        WSYNC();
-                        TPHASE(8);
-                        acl_phase<true>(L, H, lane);
-                        WSYNC();
-                        TPHASE(6);
-#ifdef GPMPC_SWEEP_VALU
-                        valu_forward(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                        mfma4_forward2(L, H, lane);
-#else
-                        mfma4_forward(L, H, lane);
-#endif
-                        WSYNC();
-                        TPHASE(9);
-                        recover_q<NV>(L, H, kq, vb, dd, dp);
-                        TPHASE(3);
-                    } else {
-                        if constexpr (kMfmaBig) {
-                            if (!mfma_backward_big(L, H, lane)) { qp_ok = false; break; }
-                            WSYNC();
-                        } else {
-                            if (!riccati_factor(L, H, lane, E)) { qp_ok = false; break; }
-                        }
-                        TPHASE(6);
-                        riccati_forward(L, H, lane);
-                        TPHASE(3);
-                        recover_q<NV>(L, H, kq, vb, dd, dp);
-                    }
-                    // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
-                    // alpha_max = 1 / max(1, max_i -dv_i / v_i)
-                    double rmax = 1.0, mua_l = 0.0;
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        if (avq(j)) {
-                            const double rl = d[j] - blo[j] - sl[j];
-                            const double ru = bup[j] - d[j] - su[j];
-                            const double ql = (dd[j] + rl) * isl[j], qu = (-dd[j] + ru) * isu[j];
-                            rmax = fmax(rmax, fmax(fmax(-ql, -qu), fmax(1.0 + ql, 1.0 + qu)));
-                        }
-                    }
-                    const double a_aff = fast_rcp(wave_max(rmax));
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        if (avq(j)) {
-                            const double rl = d[j] - blo[j] - sl[j];
-                            const double ru = bup[j] - d[j] - su[j];
-                            const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
-                            const double ql = dsl * isl[j], qu = dsu * isu[j];
-                            mua_l += ll[j] * fma(-a_aff, 1.0 + ql, 1.0) * fma(a_aff, dsl, sl[j]) +
-                                     lu[j] * fma(-a_aff, 1.0 + qu, 1.0) * fma(a_aff, dsu, su[j]);
-                        }
-                    }
-                    const double mu_aff = wave_sum(mua_l) / nc;
-                    const double sr = mu_aff / mu;
-                    const double smu = sr * sr * sr * mu;
-                    // corrector: r_ml = ll sl + dll_aff dsl_aff - sigma mu  ->  gq += (dll dsl - smu)/sl - (dlu dsu - smu)/su
-                    double dda[NV];
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        dda[j] = dd[j];
-                        if (on_q && avq(j)) {
-                            const double rl = d[j] - blo[j] - sl[j];
-                            const double ru = bup[j] - d[j] - su[j];
-                            const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
-                            const double dll = -ll[j] * fma(dsl, isl[j], 1.0);
-                            const double dlu = -lu[j] * fma(dsu, isu[j], 1.0);
-                            L.gq[k_q * NB + vb + j] += (dll * dsl - smu) * isl[j] - (dlu * dsu - smu) * isu[j];
-                        }
-                    }
-                    WSYNC();
-                    TPHASE(5);
-                    if constexpr (kCR) {
-                        cr_rhs(L, H, lane);
-                        WSYNC();
-                        cr_solve(L, H, lane);
-                        TPHASE(9);
-                        recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
-                        TPHASE(3);
-                    } else if constexpr (kMfma) {
-#ifdef GPMPC_SWEEP_VALU
-                        valu_vector_backward<0>(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                        valu_vector_backward<2>(L, H, lane);
-#else
-                        valu_vector_backward<1>(L, H, lane);
-#endif
-                        TPHASE(8);
-                        acl_phase<false>(L, H, lane);
-                        WSYNC();
-                        TPHASE(6);
-#ifdef GPMPC_SWEEP_VALU
-                        valu_forward(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                        mfma4_forward2(L, H, lane);
-#else
-                        mfma4_forward(L, H, lane);
-#endif
-                        WSYNC();
-                        TPHASE(9);
-                        recover_q<NV>(L, H, kq, vb, dd, dp);
-                        TPHASE(3);
-                    } else {
-                        riccati_vector(L, H, lane);
-                        TPHASE(6);
-                        riccati_forward(L, H, lane);
-                        TPHASE(3);
-                        recover_q<NV>(L, H, kq, vb, dd, dp);
-                    }
-                    rmax = 1.0;
-                    double dsl[NV], dsu[NV], dll[NV], dlu[NV];
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        dsl[j] = dsu[j] = dll[j] = dlu[j] = 0.0;
-                        if (avq(j)) {
-                            const double rl = d[j] - blo[j] - sl[j];
-                            const double ru = bup[j] - d[j] - su[j];
-                            const double dsla = dda[j] + rl, dsua = -dda[j] + ru;
-                            const double dlla = -ll[j] * fma(dsla, isl[j], 1.0);
-                            const double dlua = -lu[j] * fma(dsua, isu[j], 1.0);
-                            const double rml = ll[j] * sl[j] + dlla * dsla - smu;
-                            const double rmu = lu[j] * su[j] + dlua * dsua - smu;
-                            dsl[j] = dd[j] + rl;
-                            dsu[j] = -dd[j] + ru;
-                            dll[j] = (-rml - ll[j] * dsl[j]) * isl[j];
-                            dlu[j] = (-rmu - lu[j] * dsu[j]) * isu[j];
-                            const double ill = fast_rcp(ll[j]), ilu = fast_rcp(lu[j]);
-                            rmax = fmax(rmax, fmax(fmax(-dsl[j] * isl[j], -dsu[j] * isu[j]),
-                                                   fmax(-dll[j] * ill, -dlu[j] * ilu)));
-                        }
-                    }
-                    const double alpha = fmin(1.0, 0.995 * fast_rcp(wave_max(rmax)));
-#pragma unroll
-                    for (int j = 0; j < NV; ++j) {
-                        if (avq(j)) {
-                            d[j] = fma(alpha, dd[j], d[j]);
-                            sl[j] = fma(alpha, dsl[j], sl[j]);
-                            su[j] = fma(alpha, dsu[j], su[j]);
-                            ll[j] = fma(alpha, dll[j], ll[j]);
-                            lu[j] = fma(alpha, dlu[j], lu[j]);
-                        }
-                    }
-                    if (actu_q) {
-#pragma unroll
-                        for (int i = 0; i < NX; ++i) piq[i] = fma(alpha, dp[i], piq[i]);
-                    }
-                }
-            }
+            const bool qp_ok = qp_ipm<SPL, NV>(P, L, H, lane, 0, E, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
+            if constexpr (WSPL) qp_publish_step<NV>(L, H, lane, 0, d);   // B2: the full step in Dq
             qp_total += qit;
             TPHASE(2);
             if (!qp_ok) { status = kQPFailure; break; }
@@ -2863,6 +3095,7 @@ struct SqpKernel {
             for (int v = 0; v < NB; ++v) {
                 // d of variable v of this lane's stage (lane = stage layout: lanes 0..31)
                 double dv = (v < NV) ? d[v < NV ? v : 0] : 0.0;
+                if constexpr (WSPL) dv = L.Dq[(size_t)k * NB + v];
                 if constexpr (SPL) {
                     const double up = xor32_d(d[v >= NV ? v - NV : 0]);   // lane + 32 (upper lanes: unused)
                     dv = (v >= NV) ? up : dv;
@@ -2991,8 +3224,10 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
 template <int ID>
 hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
     // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
+    // (multi-wave models split the IPM state over their waves instead: WSPL)
 #ifndef GPMPC_NO_SPLIT
-    if (P.H + 1 <= 32) return launch_sqp_variant<ID, true>(P, S, io, batch, stream);
+    if constexpr (SqpKernel<ID>::NWAVES == 1)
+        if (P.H + 1 <= 32) return launch_sqp_variant<ID, true>(P, S, io, batch, stream);
 #endif
     return launch_sqp_variant<ID, false>(P, S, io, batch, stream);
 }
