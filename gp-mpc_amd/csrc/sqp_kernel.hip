@@ -855,6 +855,165 @@ struct SqpKernel {
         }
     }
 
+    // ------------------------------------------------------------------ VALU sweeps in registers (wide stages)
+    // Forward sweep dx_0 = 0, du_k = K'_k [dx_k; 1], dx_{k+1} = G'_k [dx_k; du_k; 1] with the state in
+    // registers (lane i < NX: dx[i]) and broadcast by v_readlane: every lane forms the x-part of its
+    // G' row and lanes NX..NB-1 (a = lane - NX) the input du_a from their K' row, then du is broadcast
+    // the same way.  The stage operands (one G' row, one K' row per lane) are loaded a stage ahead.
+    // Replaces riccati_forward's LDS round trip per stage; same output (dxv).
+    __device__ static void valu_forward_big(const Lds& L, int H, int lane) {
+        const int row = lane < NX ? lane : 0;
+        const int a = (lane >= NX && lane < NB) ? lane - NX : 0;
+        const double* gp = L.G + (size_t)row * GS;
+        const double* kp = L.K + (size_t)a * PS;
+        struct St { double g[GS], kr[PS]; };
+        auto load = [&](int k, St& st) {
+#pragma unroll
+            for (int j = 0; j < GS; ++j) st.g[j] = gp[(size_t)k * NX * GS + j];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) st.kr[j] = kp[(size_t)k * NU * PS + j];
+        };
+        if (lane < NX) L.dxv[lane] = 0.0;
+        double* out = (lane < NX) ? L.dxv + NX + lane : L.dummy + lane;
+        const int ost = (lane < NX) ? NX : 0;
+        double x = 0.0;
+        auto step = [&](const St& st) {
+            double xs[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) xs[j] = readlane_d(x, j);
+            double du0 = st.kr[NX], du1 = 0.0, ax0 = st.g[NB], ax1 = 0.0;
+#pragma unroll
+            for (int j = 0; j < NX; ++j) {
+                if (j & 1) {
+                    du1 = fma(st.kr[j], xs[j], du1);
+                    ax1 = fma(st.g[j], xs[j], ax1);
+                } else {
+                    du0 = fma(st.kr[j], xs[j], du0);
+                    ax0 = fma(st.g[j], xs[j], ax0);
+                }
+            }
+            const double du = du0 + du1;
+            double acc = ax0 + ax1;
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) acc = fma(st.g[NX + b2], readlane_d(du, NX + b2), acc);
+            x = acc;
+            *out = acc;
+            out += ost;
+        };
+        St s0, s1;
+        load(0, s0);
+        int k = 0;
+        for (; k + 1 < H; k += 2) {
+            load(k + 1, s1);
+            step(s0);
+            if (k + 2 < H) load(k + 2, s0);
+            step(s1);
+        }
+        if (k < H) step(s0);
+        WSYNC();
+    }
+
+    // Corrector vector sweep (HPIPM's solve with the stored factorisation), state in registers:
+    //   pv = t_k + p_{k+1} (t_k = P_{k+1} c_k for all stages in parallel first),
+    //   lane j < NB: s_j = gq_kj + sum_l G'_k[l][j] pv_l   (x-part of p_k for j < NX, gu_a for j = NX + a),
+    //   p_k = s_x + K_k' gu (lanes < NX),  kff_k = -Ru_k^-1 gu (lanes NX..NB-1),
+    // with pv and gu broadcast by v_readlane.  Same outputs as riccati_vector (p in P', kff in K').
+    // Scratch: t aliases hq (rewritten before the next factorisation).
+    __device__ static void valu_vector_big(const Lds& L, int H, int lane) {
+        double* T = L.hq;
+        const int n = H * NX;
+        auto t_entry = [&](int e) {
+            const int k = e / NX, i = e - k * NX;
+            const double* Pn = L.P + (size_t)(k + 1) * PP;
+            const double* G = L.G + (size_t)k * NX * GS;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
+            return acc;
+        };
+        for (int e0 = lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            T[e0] = a0;
+            if (has1) T[e1] = a1;
+        }
+        WSYNC();
+        const int col = lane < NB ? lane : 0;
+        const int row = lane < NX ? lane : 0;
+        const int a = (lane >= NX && lane < NB) ? lane - NX : 0;
+        struct St { double g[NX], kc[NU], ri[NU], gq, t; };
+        auto load = [&](int k, St& st) {
+            const double* G = L.G + (size_t)k * NX * GS + col;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) st.g[l] = G[l * GS];
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                st.kc[b2] = L.K[(size_t)k * NU * PS + b2 * PS + row];
+                st.ri[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
+            }
+            st.gq = L.gq[k * NB + col];
+            st.t = T[k * NX + row];
+        };
+        double p = (lane < NX) ? L.gq[H * NB + lane] : 0.0;
+        if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
+        double* pout = (lane < NX) ? L.P + (size_t)(H - 1) * PP + PO + lane : L.dummy + lane;
+        const int pst = (lane < NX) ? PP : 0;
+        double* kout = (lane >= NX && lane < NB) ? L.K + (size_t)(H - 1) * NU * PS + a * PS + NX : L.dummy + lane;
+        const int kst = (lane >= NX && lane < NB) ? NU * PS : 0;
+        auto step = [&](int k, const St& st) {
+            const double pv = st.t + p;
+            double s0 = st.gq, s1 = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                const double pl = readlane_d(pv, l);
+                if (l & 1) s1 = fma(st.g[l], pl, s1);
+                else s0 = fma(st.g[l], pl, s0);
+            }
+            const double sj = s0 + s1;
+            double pn = sj, kf = 0.0;
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                const double gu = readlane_d(sj, NX + b2);
+                pn = fma(st.kc[b2], gu, pn);
+                kf = fma(st.ri[b2], gu, kf);
+            }
+            p = pn;
+            if (k >= 1) *pout = pn;   // p_0 is not needed
+            pout -= pst;
+            *kout = -kf;
+            kout -= kst;
+        };
+        St s0, s1;
+        load(H - 1, s0);
+        int k = H - 1;
+        for (; k >= 1; k -= 2) {
+            load(k - 1, s1);
+            step(k, s0);
+            if (k >= 2) load(k - 2, s0);
+            step(k - 1, s1);
+        }
+        if (k == 0) step(0, s0);
+        WSYNC();
+    }
+
+    // sweeps of the wide (non-MFMA) path: the register versions above; -DGPMPC_SWEEP_LDS keeps the
+    // LDS-staged riccati_forward / riccati_vector
+    __device__ static void forward_big(const Lds& L, int H, int lane) {
+#ifdef GPMPC_SWEEP_LDS
+        riccati_forward(L, H, lane);
+#else
+        valu_forward_big(L, H, lane);
+#endif
+    }
+    __device__ static void vector_big(const Lds& L, int H, int lane) {
+#ifdef GPMPC_SWEEP_LDS
+        riccati_vector(L, H, lane);
+#else
+        valu_vector_big(L, H, lane);
+#endif
+    }
+
     // Per-lane step of stage k from the Riccati solution: dd = [dx_k; du_k] and dpi_k.
     __device__ static void recover_step(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
         const bool on = lane <= H;
@@ -2430,7 +2589,10 @@ struct SqpKernel {
     __device__ static bool xall(const Lds& L, int lane, int wv, int& par, bool ok) {
         return xmax(L, lane, wv, par, ok ? 0.0 : 1.0) == 0.0;
     }
+    // WSPL: wave owning row i of the dynamics residual
+    __host__ __device__ static constexpr int xrow_of(int i) { return i / ((NX + NWAVES - 1) / NWAVES); }
     // dynamics residual of stage kq; WSPL: the waves exchange their parts of the step vector in LDS
+    // and each computes its rows (its share of the max norm and of column NB of G')
     template <bool SPL, int NV>
     __device__ static void dyn_residual_x(const Lds& L, int H, int kq, int vb, const double (&d)[NV],
                                           const double (&c)[NX], double (&r)[NX]) {
@@ -2443,11 +2605,16 @@ struct SqpKernel {
             const double* dk = L.Dq + (size_t)min(kq, H) * NB;
             const double* dn = L.Dq + (size_t)min(kq + 1, H) * NB;
             const double* G = L.G + (size_t)min(kq, H - 1) * NX * GS;
+            const int wv = threadIdx.x >> 6;
             double df[NB];
 #pragma unroll
             for (int v = 0; v < NB; ++v) df[v] = dk[v];
 #pragma unroll
-            for (int i = 0; i < NX; ++i) {
+            for (int i = 0; i < NX; ++i) {   // this wave's rows (xrow_of); the others are 0 here
+                if (xrow_of(i) != wv) {
+                    r[i] = 0.0;
+                    continue;
+                }
                 double acc = dn[i] - c[i];
 #pragma unroll
                 for (int j = 0; j < NB; ++j) acc = fma(-G[i * GS + j], df[j], acc);
@@ -2568,9 +2735,10 @@ struct SqpKernel {
                 mu /= nc;
                 if (!(mu == mu) || !(m_res == m_res)) { qp_ok = false; break; }
                 if (m_res <= P.qp_tol && mu <= P.qp_tol) break;
-                if (actu_q && !hi_half && wv == 0) {
+                if (actu_q && !hi_half) {
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
+                    for (int i = 0; i < NX; ++i)
+                        if (!WSPL || xrow_of(i) == wv) L.G[(size_t)kq * NX * GS + i * GS + NB] = -rp[i];
                 }
                 XSYNC();
                 TPHASE(4);
@@ -2615,7 +2783,7 @@ struct SqpKernel {
                             rok = riccati_factor(L, H, lane, E);
                         }
                         TPHASE(6);
-                        if (rok) riccati_forward(L, H, lane);
+                        if (rok) forward_big(L, H, lane);
                     }
                     if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
                     if (!rok) { qp_ok = false; break; }
@@ -2697,9 +2865,9 @@ struct SqpKernel {
                     TPHASE(3);
                 } else {
                     if (wv == 0) {
-                        riccati_vector(L, H, lane);
+                        vector_big(L, H, lane);
                         TPHASE(6);
-                        riccati_forward(L, H, lane);
+                        forward_big(L, H, lane);
                     }
                     XSYNC();
                     TPHASE(3);
