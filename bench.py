@@ -130,8 +130,10 @@ def parse_args(argv=None):
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
-    ap.add_argument("--variance", choices=["exact", "love"], default="exact",
-                    help="tightening variance: exact, or LOVE (gpytorch fast_pred_var, rank 100) above 800 rows")
+    ap.add_argument("--variance", choices=["exact", "love"], default="love",
+                    help="tightening variance: 'love' = the reference's gpytorch fast_pred_var (exact Cholesky up "
+                         "to 800 training rows, rank-100 Lanczos root above; configs 2-3 are exact either way), "
+                         "'exact' = L^-1 k at every size")
     ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
                     help="tools/pmc_summary.py output of the same command (roofline.traffic)")
     ap.add_argument("--dry-run", action="store_true",
@@ -143,7 +145,8 @@ def workload_name(spec, args):
     N, H, B = args.n_train, args.horizon, args.batch
     return (f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}"
             f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}"
-            f"{', LOVE variance' if getattr(args, 'variance', 'exact') == 'love' else ''}, "
+            f"{', LOVE variance' if getattr(args, 'variance', 'exact') == 'love' and N > 800 else ''}"
+            f"{', exact variance' if getattr(args, 'variance', 'exact') == 'exact' and N > 800 else ''}, "
             f"{B} instances per GPU, closed loop")
 
 

@@ -36,7 +36,7 @@ class GPMPC:
                  horizon: int = 25, q_mpc: list | None = None, r_mpc: list | None = None, sparse_gp: bool = False,
                  prob: float = 0.955, max_gp_samples: int = 30, seed: int = 1337, device: str = "cuda",
                  output_dir: Path | None = None, batch: int = 1, variance_inputs: str = "reference",
-                 variance: str = "exact", **solver_kw):
+                 variance: str = "love", **solver_kw):
         spec = (symbolic_model if isinstance(symbolic_model, ModelSpec) else get_spec(symbolic_model)).copy()
         # "reference": the variance input map of `gpmpc/gpmpc.py:437-444` (for quad3d it indexes the
         # full state-input vector with the GP-input-space indices); "dynamics": each GP's own inputs
@@ -45,8 +45,10 @@ class GPMPC:
         elif variance_inputs != "reference":
             raise ValueError("variance_inputs must be 'reference' or 'dynamics'")
         self.model = spec
-        # tightening variance: "exact" (L^-1 k), or "love": gpytorch fast_pred_var's Lanczos root
-        # above 800 training rows, as the reference's propagate_constraint_limits (gpmpc.py:442-444)
+        # tightening variance.  Default "love": what the reference computes -- its
+        # propagate_constraint_limits runs under gpytorch.settings.fast_pred_var() (gpmpc.py:442-444),
+        # i.e. the exact Cholesky variance up to gpytorch's max_cholesky_size (800 training rows)
+        # and the rank-100 Lanczos (LOVE) root above it; "exact": L^-1 k at every size.
         self.variance = variance
         if q_mpc is not None:
             spec.q_diag = np.asarray(q_mpc, dtype=np.float64)
