@@ -5,7 +5,9 @@
 #    rocprofv3 kernel trace/stats, one SQ PMC pass and the FETCH_SIZE / WRITE_SIZE passes of the
 #    same command (tools/driver_prof.sh)
 # 2. in-kernel phase breakdown (timing build) of configs 3 and 5
-# 3. the other BASELINE configs (one shard per GPU), each with its CPU baseline (1 core, all cores)
+# 3. the other BASELINE configs (one shard per GPU), each with its CPU baseline (1 core, all cores);
+#    configs 4 and 5 at the default (the reference's gpytorch fast_pred_var: LOVE above 800 rows) and
+#    with --variance exact
 set -e
 OUT=${1:?outdir}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -19,3 +21,7 @@ timeout -k 10 240 python3 -u bench.py --model cartpole --n-train 50 --horizon 20
 timeout -k 10 300 python3 -u bench.py --n-train 1000 --steps 20 --warmup 5 > "$OUT/config4.json" 2>> "$OUT/bench.err"
 timeout -k 10 600 python3 -u bench.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
     --var-inputs dynamics --steps 20 --warmup 5 > "$OUT/config5.json" 2>> "$OUT/bench.err"
+timeout -k 10 300 python3 -u bench.py --n-train 1000 --steps 20 --warmup 5 --variance exact --no-cpu-baseline \
+    > "$OUT/config4_exact.json" 2>> "$OUT/bench.err"
+timeout -k 10 600 python3 -u bench.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
+    --var-inputs dynamics --steps 20 --warmup 5 --variance exact --no-cpu-baseline > "$OUT/config5_exact.json" 2>> "$OUT/bench.err"
