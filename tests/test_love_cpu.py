@@ -62,3 +62,23 @@ def test_love_threshold_follows_gpytorch_cholesky_size():
     from gpmpc.gp import LOVE_CHOLESKY_ROWS
 
     assert LOVE_CHOLESKY_ROWS == 800   # gpytorch.settings.max_cholesky_size default
+
+
+def test_default_tightening_variance_is_the_references_fast_pred_var():
+    """GPMPC and bench.py default to variance='love': the reference's propagate_constraint_limits
+    runs under gpytorch.settings.fast_pred_var() (gpmpc/gpmpc.py:442-444), i.e. exact up to 800
+    training rows (BatchSolver applies the Lanczos root only above LOVE_CHOLESKY_ROWS)."""
+    import inspect
+    import sys
+    from pathlib import Path
+
+    from gpmpc.gpmpc import GPMPC
+    from gpmpc.models import get_spec
+
+    assert inspect.signature(GPMPC.__init__).parameters["variance"].default == "love"
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    assert bench.parse_args([]).variance == "love"
+    assert "LOVE" not in bench.workload_name(get_spec("quad2d"), bench.parse_args([]))   # N = 200: exact
+    assert "LOVE" in bench.workload_name(get_spec("quad2d"), bench.parse_args(["--n-train", "1000"]))
