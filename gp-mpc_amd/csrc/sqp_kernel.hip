@@ -321,7 +321,13 @@ struct SqpKernel {
     // Waves per instance.  The wide model (quad3d) needs more LDS than two instances per CU can
     // have, so its CU's other SIMDs would idle: three GP helper waves take a share of every GP
     // tile pass (gp_tiles over tiles w, w + 4, ...), the main wave runs everything else.
-    static constexpr int NWAVES = (NB + 1 > 16) ? 4 : 1;
+#ifdef GPMPC_W2
+    static constexpr bool kW2 = true;
+#else
+    static constexpr bool kW2 = false;
+#endif
+    // -DGPMPC_W2: two waves per instance for the single-tile models with an even stage width (quad2d)
+    static constexpr int NWAVES = (NB + 1 > 16) ? 4 : ((kW2 && NB % 2 == 0) ? 2 : 1);
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
 
@@ -363,8 +369,10 @@ struct SqpKernel {
             return base + reg;
         }
         if (kMfma) {
-            const size_t acl = (size_t)H * NX * PS;            // closed-loop A'_k (tightening scratch aliases it)
-            return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H));
+            // closed-loop A'_k (the tightening scratch and, WSPL, the step-vector exchange Dq alias it)
+            const size_t acl = (size_t)H * NX * PS;
+            return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H))
+                   + (NWAVES > 1 ? 16 : 0);                      // WSPL reduction slots (xs)
         }
         return common + p_region(H)                             // P'_k (packed) | GP scratch
                + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
@@ -408,6 +416,12 @@ struct SqpKernel {
             L.Acl = s;
             L.cd = s;
             L.Sig = s + (size_t)H * NUNC;
+            if constexpr (NWAVES > 1) {   // Dq: live only inside an IPM iteration's residual phase
+                L.Dq = s;
+                const size_t acl = (size_t)H * NX * PS;
+                s += acl > tight_scratch(H) ? acl : tight_scratch(H);
+                L.xs = s;
+            }
         } else {
             L.P = s;   s += p_region(H);
             L.W = s;   s += (size_t)NX * GS;
@@ -1392,28 +1406,38 @@ struct SqpKernel {
         const int srui_st = rst ? NU * NU : 0;
         double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
         bool pend = false;
+        // DIAG (tools/ric_micro.hip): bit 3 drops only the P' stores, bit 4 flushes without the
+        // scheduling barriers, bit 5 flushes after the M' products instead of the W' products
         auto flush = [&]() {
+            if constexpr ((DIAG & 8) == 0) {
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                *sp[r] = pend_p[r];
-                sp[r] -= sp_st[r];
+                for (int r = 0; r < 2; ++r) {
+                    *sp[r] = pend_p[r];
+                    sp[r] -= sp_st[r];
+                }
             }
             *sk = pend_k;
             sk -= sk_st;
             *srui = pend_r;
             srui -= srui_st;
         };
-        auto stage = [&](const Stage& sd) {
-            f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
-            w = mfma64(pn[1], sd.g[1], w);
-            if constexpr ((DIAG & 1) == 0) {
+        auto flush_at = [&]() {
+            if constexpr ((DIAG & 16) != 0) {
+                if (pend) flush();
+            } else {
                 __builtin_amdgcn_sched_barrier(0);
                 if (pend) flush();
                 __builtin_amdgcn_sched_barrier(0);
-                pend = true;
             }
+            pend = true;
+        };
+        auto stage = [&](const Stage& sd) {
+            f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
+            w = mfma64(pn[1], sd.g[1], w);
+            if constexpr ((DIAG & 1) == 0 && (DIAG & 32) == 0) flush_at();
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
             m = mfma64(sd.g[1], w[1], m);
+            if constexpr ((DIAG & 1) == 0 && (DIAG & 32) != 0) flush_at();
             double Ru[NU][NU];
 #pragma unroll
             for (int a = 0; a < NU; ++a)
@@ -2755,20 +2779,27 @@ struct SqpKernel {
                     recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else if constexpr (kMfma) {
-                    if (!mfma_backward_h(L, H, lane)) { qp_ok = false; break; }
-                    WSYNC();
-                    TPHASE(8);
-                    acl_phase<true>(L, H, lane);
-                    WSYNC();
-                    TPHASE(6);
+                    bool rok = true;
+                    if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
+                        rok = mfma_backward_h(L, H, lane);
+                        WSYNC();
+                        TPHASE(8);
+                        if (rok) acl_phase<true>(L, H, lane);
+                        WSYNC();
+                        TPHASE(6);
+                        if (rok) {
 #ifdef GPMPC_SWEEP_VALU
-                    valu_forward(L, H, lane);
+                            valu_forward(L, H, lane);
 #elif defined(GPMPC_SWEEP4)
-                    mfma4_forward2(L, H, lane);
+                            mfma4_forward2(L, H, lane);
 #else
-                    mfma4_forward(L, H, lane);
+                            mfma4_forward(L, H, lane);
 #endif
-                    WSYNC();
+                        }
+                        WSYNC();
+                    }
+                    if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
+                    if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
@@ -2841,25 +2872,28 @@ struct SqpKernel {
                     recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else if constexpr (kMfma) {
+                    if (wv == 0) {
 #ifdef GPMPC_SWEEP_VALU
-                    valu_vector_backward<0>(L, H, lane);
+                        valu_vector_backward<0>(L, H, lane);
 #elif defined(GPMPC_SWEEP4)
-                    valu_vector_backward<2>(L, H, lane);
+                        valu_vector_backward<2>(L, H, lane);
 #else
-                    valu_vector_backward<1>(L, H, lane);
+                        valu_vector_backward<1>(L, H, lane);
 #endif
-                    TPHASE(8);
-                    acl_phase<false>(L, H, lane);
-                    WSYNC();
-                    TPHASE(6);
+                        TPHASE(8);
+                        acl_phase<false>(L, H, lane);
+                        WSYNC();
+                        TPHASE(6);
 #ifdef GPMPC_SWEEP_VALU
-                    valu_forward(L, H, lane);
+                        valu_forward(L, H, lane);
 #elif defined(GPMPC_SWEEP4)
-                    mfma4_forward2(L, H, lane);
+                        mfma4_forward2(L, H, lane);
 #else
-                    mfma4_forward(L, H, lane);
+                        mfma4_forward(L, H, lane);
 #endif
-                    WSYNC();
+                        WSYNC();
+                    }
+                    XSYNC();
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
@@ -3372,8 +3406,12 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
     return hipGetLastError();
 }
 
+// One wave per SIMD (the instance owns the register file), except the two-wave quad2d variant
+// (GPMPC_W2), which must fit two waves per SIMD.
+template <int ID>
+constexpr int kWavesPerEU = (SqpKernel<ID>::NWAVES == 2) ? 2 : 1;
 template <int ID, bool SPL>
-__global__ __launch_bounds__(64 * SqpKernel<ID>::NWAVES) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
+__global__ __launch_bounds__(64 * SqpKernel<ID>::NWAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<ID>, kWavesPerEU<ID>))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
     SqpKernel<ID>::template run<SPL>(P, S, io);
 }
 

@@ -54,6 +54,10 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
         if constexpr (V == 4) KQ::valu_forward(L, H, lane);
         if constexpr (V == 6) KQ::valu_vector_backward<1>(L, H, lane);
         if constexpr (V == 15) KQ::valu_vector_backward<2>(L, H, lane);
+        if constexpr (V == 16) KQ::mfma_backward_h<8>(L, H, lane);
+        if constexpr (V == 17) KQ::mfma_backward_h<16>(L, H, lane);
+        if constexpr (V == 18) KQ::mfma_backward_h<32>(L, H, lane);
+        if constexpr (V == 19) KQ::mfma_backward_h<48>(L, H, lane);
         if constexpr (V == 5) { double v = (double)r; for (int q = 0; q < H; ++q) v = wave_sum(v) * 1e-3; L.dummy[lane] = v; }
         WSYNC();
     }
@@ -228,6 +232,10 @@ int main() {
     run<13>("factor, homog no st", H, B, reps, d_out, d_sink);
     run<14>("forward (4-chain)", H, B, reps, d_out, d_sink);
     run<15>("backward (vec 4-chain)", H, B, reps, d_out, d_sink);
+    run<16>("factor h, no P' st", H, B, reps, d_out, d_sink);
+    run<17>("factor h, no sched_b", H, B, reps, d_out, d_sink);
+    run<18>("factor h, st after M", H, B, reps, d_out, d_sink);
+    run<19>("factor h, after M nsb", H, B, reps, d_out, d_sink);
     check(H);
     return 0;
 }
