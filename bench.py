@@ -357,9 +357,11 @@ def run_gpu(args, rank, local_rank, world):
                                  "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
                                  "Riccati recursion"},
             "roofline_variance": None if var_tf is None else {
-                "kernel": (f"gp_var_tri_kernel<{(N + 15) // 16},true>"
-                           if (N + 15) // 16 <= 16 and not any(getattr(solver, "love_ranks", None) or [])
-                           else "gp_post_kernel<true>"),
+                "kernel": ((f"gp_love_kernel<{max((r + 15) // 16 for r in solver.love_ranks if r)},true> "
+                            f"(LOVE root rank {max(r for r in solver.love_ranks if r)})")
+                           if any(getattr(solver, "love_ranks", None) or [])
+                           else (f"gp_var_tri_kernel<{(N + 15) // 16},true>" if (N + 15) // 16 <= 16
+                                 else "gp_post_kernel<true>")),
                 "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},
             "exp_ceiling": {"exps_per_launch": exps_launch, "achieved_per_s": exps_launch / (sqp_ms * 1e-3),

@@ -288,6 +288,108 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
     }
 }
 
+// ---------------------------------------------------------------------------- variance, LOVE root
+// var(z) = sf2 - ||R^T k(z, X)||^2 (+ sn2) with the dense LOVE root R [npad][16 NTC]
+// (gpytorch fast_pred_var; NTC = the widest root of the launch in 16-column tiles, 7 for the
+// rank-100 roots of configs 4/5): 2 N (16 NTC) flops per point on the matrix core against one exp
+// per training row.  No LDS and no barriers: one wavefront = 16
+// points, K-steps of four training rows (lane (kq, lc): point lc, row 4s + kq) on
+// v_mfma_f64_16x16x4_f64, four K-steps per round with their exps interleaved (exp_rbf_n) and the
+// next round's training rows and root entries loaded a round ahead (the blocks of one GP run
+// together, so its root, 3.6 MB at N = 4000 and 112 columns, streams through L2 once per wave
+// generation).  No 16-tile accumulator array and no LDS: 2-3 waves per SIMD hide the loads, against
+// one barrier per 16-row panel in gp_post_kernel.  sf2 is applied to the squared norm (sf2^2), not
+// to every kernel value.
+constexpr int kLoveWaves = 4;
+template <int NTC, bool FROM_STATE>
+__global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) {
+    const GPDev& g = pb.g[blockIdx.y];
+    const PostArgs& a = pb.a[blockIdx.y];
+    const int npad = pb.npad[blockIdx.y];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int p0 = (blockIdx.x * kLoveWaves + wave) * 16;
+    if (p0 >= a.P) return;   // wave-uniform
+    const int lc = lane & 15, kq = lane >> 4;
+    const int p = p0 + lc;
+    double z[3];
+    load_point<FROM_STATE>(a, p < a.P ? p : a.P - 1, z);
+    const double c = -0.5 * g.inv_ell2;
+    const double4* rows = reinterpret_cast<const double4*>(g.vrows);
+    const int NC = g.vroot_cols, ntc = NC / 16;   // this GP's root width (<= 16 NTC)
+    const double* Rl = g.vroot + kq * NC + lc;   // this lane's B entries: R[16 s4 + 4 ks + kq][16 t + lc]
+    const int nv = g.nv, nround = npad / 16;
+    struct Round { double4 x[4]; double b[4][NTC]; };
+    auto load = [&](int s4, Round& rd) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int i = 16 * s4 + 4 * ks + kq;
+            rd.x[ks] = rows[i < nv ? i : 0];
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) rd.b[ks][t] = (t < ntc) ? Rl[(size_t)(16 * s4 + 4 * ks) * NC + 16 * t] : 0.0;
+        }
+    };
+    f64x4 acc[NTC];
+#pragma unroll
+    for (int t = 0; t < NTC; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    auto round = [&](int s4, const Round& rd) {
+        double kv[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const double4 r = rd.x[ks];
+            const double d0 = r.x - z[0], d1 = r.y - z[1], d2 = r.z - z[2];
+            kv[ks] = c * fma(d0, d0, fma(d1, d1, d2 * d2));   // unused input dims are zero on both sides
+        }
+        exp_rbf_n<4>(kv);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const double kvm = (16 * s4 + 4 * ks + kq < nv) ? kv[ks] : 0.0;
+#pragma unroll
+            for (int t = 0; t < NTC; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kvm, rd.b[ks][t], acc[t], 0, 0, 0);
+        }
+    };
+    // (measured on configs 4/5: this plain form beats unconditional clamped prefetches, with or
+    // without scheduling barriers around them)
+    Round r0, r1;
+    load(0, r0);
+    int s4 = 0;
+    for (; s4 + 1 < nround; s4 += 2) {
+        load(s4 + 1, r1);
+        round(s4, r0);
+        if (s4 + 2 < nround) load(s4 + 2, r0);
+        round(s4 + 1, r1);
+    }
+    if (s4 < nround) round(s4, r0);
+    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NTC; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sq[r] = fma(acc[t][r], acc[t][r], sq[r]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sq[r] = dpp_row_sum(sq[r]);   // over the 16 column lanes
+    if (lc == 0) {
+        const double sf2sq = g.sf2 * g.sf2;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int pr = p0 + kq + 4 * r;
+            if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = g.sf2 - sf2sq * sq[r] + (a.with_noise ? g.sn2 : 0.0);
+        }
+    }
+}
+
+template <bool FROM_STATE, int NTC = 1>
+hipError_t launch_love(const PostBatch& pb, int ntc, hipStream_t stream) {
+    if constexpr (NTC <= 8) {
+        if (ntc == NTC) {
+            int blocks = 0;
+            for (int q = 0; q < pb.n; ++q) blocks = max(blocks, (pb.a[q].P + 16 * kLoveWaves - 1) / (16 * kLoveWaves));
+            hipLaunchKernelGGL((gp_love_kernel<NTC, FROM_STATE>), dim3(blocks, pb.n), dim3(64 * kLoveWaves), 0, stream, pb);
+            return hipGetLastError();
+        }
+        return launch_love<FROM_STATE, NTC + 1>(pb, ntc, stream);
+    }
+    return hipErrorInvalidValue;
+}
+
 template <bool FROM_STATE, int NT = 1>
 hipError_t launch_var_tri(const PostBatch& pb, int ntile, int blocks, hipStream_t stream) {
     if constexpr (NT <= kMaxCT) {
@@ -320,6 +422,17 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
         }
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
+#ifndef GPMPC_LOVE_POST
+    bool love = true;   // every entry variance-only with a LOVE root of <= 128 columns
+    int wmax = 0;
+    for (int q = 0; q < pb.n; ++q) {
+        love = love && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].vroot != nullptr &&
+               pb.g[q].vroot_cols % 16 == 0 && pb.g[q].vroot_cols <= 128;
+        wmax = max(wmax, pb.g[q].vroot_cols);
+    }
+    if (love)
+        return from_state ? launch_love<true>(pb, wmax / 16, stream) : launch_love<false>(pb, wmax / 16, stream);
+#endif
     bool tri = true;   // every entry variance-only with the same npad <= 256
     for (int q = 0; q < pb.n; ++q)
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&
