@@ -2684,7 +2684,7 @@ struct SqpKernel {
     // dynamics residual) in, the step d, the bound multipliers and piq (dynamics multipliers of
     // stage kq) out.  Every wave of the instance calls it (WSPL) with the same control flow.
     template <bool SPL, int NV>
-    __device__ static bool qp_ipm(const ProblemDev& P, const Lds& L, int H, int lane, int wv, const Entries& E,
+    __device__ static bool qp_ipm(const ProblemDev& P, const StateDev& S, int b, const Lds& L, int H, int lane, int wv, const Entries& E,
                                   const double (&blo)[NV], const double (&bup)[NV], const double (&gv)[NV],
                                   const double (&hd)[NV], double (&d)[NV], const double (&cqq)[NX], double (&ll)[NV],
                                   double (&lu)[NV], double (&piq)[NX], int& qit_out, Tm& tm) {
@@ -2705,6 +2705,46 @@ struct SqpKernel {
         (void)tm;
 #endif
         double sl[NV], su[NV];
+#ifndef GPMPC_QP_WARM_PIQ
+#define GPMPC_QP_WARM_PIQ 1
+#endif
+#if defined(GPMPC_QP_WARM_PI)
+        // experiment: only the dynamics multipliers warm-started, bound multipliers and slacks cold
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const bool av = avq(j);
+            sl[j] = av ? fmax(-blo[j], 1e-2) : 1.0;
+            su[j] = av ? fmax(bup[j], 1e-2) : 1.0;
+            ll[j] = av ? P.qp_mu0 * fast_rcp(sl[j]) : 0.0;
+            lu[j] = av ? P.qp_mu0 * fast_rcp(su[j]) : 0.0;
+        }
+        {
+            const double* pq = S.pi + ((size_t)b * H + min(kq, H - 1)) * NX;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) piq[i] = actu_q ? pq[i] : 0.0;
+        }
+#elif defined(GPMPC_QP_WARM)
+        // warm start (acados qp_solver_warm_start-like; experiment): slacks at the current bound
+        // distances, bound and dynamics multipliers from the last QP solution (acados memory),
+        // all floored at GPMPC_QP_WARM
+        {
+            const double fl = GPMPC_QP_WARM;
+            const double* lq = S.lam + ((size_t)b * (H + 1) + k_q) * 2 * NB + vb;
+#pragma unroll
+            for (int j = 0; j < NV; ++j) {
+                const bool av = avq(j);
+                sl[j] = av ? fmax(-blo[j], fl) : 1.0;
+                su[j] = av ? fmax(bup[j], fl) : 1.0;
+                ll[j] = av ? fmax(lq[j < NB - vb ? j : 0], fl) : 0.0;
+                lu[j] = av ? fmax(lq[NB + (j < NB - vb ? j : 0)], fl) : 0.0;
+            }
+            const double* pq = S.pi + ((size_t)b * H + min(kq, H - 1)) * NX;
+#pragma unroll
+            for (int i = 0; i < NX; ++i) piq[i] = (actu_q && GPMPC_QP_WARM_PIQ) ? pq[i] : 0.0;
+        }
+#else
+        (void)S;
+        (void)b;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const bool av = avq(j);
@@ -2715,6 +2755,7 @@ struct SqpKernel {
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) piq[i] = 0.0;
+#endif
         bool qp_ok = true;
         int qit = 0, par = 0;
         TPHASE(3);
@@ -2975,7 +3016,7 @@ struct SqpKernel {
                     qp_setup_pub<NV>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq);
                     Tm tm{};
                     int qit = 0;
-                    const bool ok = qp_ipm<false, NV>(P, L, H, lane, w, decode(lane), blo, bup, gv, hd, d, cqq, ll, lu,
+                    const bool ok = qp_ipm<false, NV>(P, S, b, L, H, lane, w, decode(lane), blo, bup, gv, hd, d, cqq, ll, lu,
                                                       piq, qit, tm);
                     if (ok && lane <= H) {   // this wave's bound multipliers (acados memory)
                         double* lam_q = S.lam + ((size_t)b * (H + 1) + lane) * 2 * NB;
@@ -3276,7 +3317,7 @@ struct SqpKernel {
                 }
             }
             int qit = 0;
-            const bool qp_ok = qp_ipm<SPL, NV>(P, L, H, lane, 0, E, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
+            const bool qp_ok = qp_ipm<SPL, NV>(P, S, b, L, H, lane, 0, E, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
             if constexpr (WSPL) qp_publish_step<NV>(L, H, lane, 0, d);   // B2: the full step in Dq
             qp_total += qit;
             TPHASE(2);
