@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -62,6 +63,9 @@ struct gpmpc_handle {
     // device state
     double *x = nullptr, *u = nullptr, *pi = nullptr, *lam = nullptr, *var = nullptr, *tight = nullptr;
     int32_t* has_prev = nullptr;
+    double* lin = nullptr;          // linearisation cache of the stored iterate (StateDev::lin)
+    int32_t* lin_tag = nullptr;
+    bool lin_cache = true;
     double* traj = nullptr;
     double* plant_params = nullptr;
     double* tgain = nullptr;        // [H][nb][n_unc] tightening gain table (ProblemDev::tgain)
@@ -95,15 +99,22 @@ static hipEvent_t take_event(gpmpc_handle* h) {
     return e;
 }
 
+// Invalidate every instance's linearisation cache (StateDev::lin): the iterate, the GPs or the
+// model changed.  Tags written by earlier launches no longer match the new generation.
+static void bump_lin(gpmpc_handle* h) {
+    if (++h->P.lin_gen <= 0) h->P.lin_gen = 1;
+}
+
 static void free_handle(gpmpc_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (auto* v : {&h->ev_var, &h->ev_sqp})
         for (auto& pr : *v) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
-    for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain})
+    for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain, h->lin})
         if (p) (void)hipFree(p);
     if (h->has_prev) (void)hipFree(h->has_prev);
+    if (h->lin_tag) (void)hipFree(h->lin_tag);
     if (h->scratch_i) (void)hipFree(h->scratch_i);
     if (h->scratch_d) (void)hipFree(h->scratch_d);
     for (int g = 0; g < kMaxGP; ++g) {
@@ -152,6 +163,8 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
         {(void**)&h->var, B * H * md.ngp * sizeof(double)},
         {(void**)&h->tight, B * (H + 1) * h->nb * sizeof(double)},
         {(void**)&h->has_prev, B * sizeof(int32_t)},
+        {(void**)&h->lin, B * H * md.nx * (h->nb + 1) * sizeof(double)},
+        {(void**)&h->lin_tag, B * sizeof(int32_t)},
         {(void**)&h->plant_params, kMaxParams * sizeof(double)},
         {(void**)&h->scratch_i, 2 * B * sizeof(int32_t)},
         {(void**)&h->scratch_d, 4 * B * sizeof(double)},
@@ -179,6 +192,11 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.qp_max_iter = 50;   // acados qp_solver_iter_max default
     P.qp_tol = 1e-8;     // HPIPM default residual tolerances (acados leaves qp_tol unset, gpmpc.py:257-263)
     P.qp_mu0 = 1.0;
+    P.lin_gen = 1;   // tags start at 0: nothing cached
+    {
+        const char* ev = std::getenv("GPMPC_LIN_CACHE");   // "0": recompute every linearisation (A/B)
+        h->lin_cache = !(ev && ev[0] == '0');
+    }
     const size_t lds = sqp_lds_bytes(model_id, horizon);
     if (lds > 160 * 1024) {
         free_handle(h);
@@ -218,6 +236,7 @@ gpmpc_status gpmpc_set_model(gpmpc_handle* h, const double* params, int32_t n_pa
     }
     P.uh = uh;
     P.cost_scale = cost_scaling ? dt : 1.0;
+    bump_lin(h);
     h->model_set = true;
     return GPMPC_OK;
 }
@@ -341,6 +360,7 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
     g.sn2 = noise;
     h->gp_npad[gp_id] = npad;
     h->gp_set[gp_id] = true;
+    bump_lin(h);
     return GPMPC_OK;
 }
 
@@ -382,6 +402,7 @@ gpmpc_status gpmpc_use_gp(gpmpc_handle* h, int32_t enabled) {
     if (enabled)
         for (int g = 0; g < h->md.ngp; ++g)
             if (!h->gp_set[g]) return fail(GPMPC_ERR_STATE, "GP " + std::to_string(g) + " not set");
+    if (h->P.use_gp != (enabled ? 1 : 0)) bump_lin(h);
     h->P.use_gp = enabled ? 1 : 0;
     return GPMPC_OK;
 }
@@ -452,6 +473,7 @@ gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, 
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
     HIPCHK(hipMemsetAsync(h->has_prev, 0, B * sizeof(int32_t), s));
+    bump_lin(h);
     if (reset_iterate) {
         HIPCHK(hipMemsetAsync(h->x, 0, B * (H + 1) * h->md.nx * sizeof(double), s));
         HIPCHK(hipMemsetAsync(h->u, 0, B * H * h->md.nu * sizeof(double), s));
@@ -470,6 +492,7 @@ gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_d
     const size_t B = batch, H = h->H;
     HIPCHK(hipMemcpyAsync(h->x, x_dev, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->u, u_dev, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
+    bump_lin(h);
     HIPCHK(hipMemsetAsync(h->pi, 0, B * H * h->md.nx * sizeof(double), s));
     HIPCHK(hipMemsetAsync(h->lam, 0, B * (H + 1) * 2 * h->nb * sizeof(double), s));
     return GPMPC_OK;
@@ -528,7 +551,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         }
     }
     // 2. the SQP step
-    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight};
+    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag};
     StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing, h->stats};
     // optional outputs go to handle-owned scratch when NULL
     if (!io.sqp_iter) io.sqp_iter = h->scratch_i;

@@ -74,6 +74,9 @@ struct ProblemDev {
     // SQP / QP options (gpmpc.py:257-263; acados default tolerances)
     int32_t max_iter, qp_max_iter;
     double tol_stat, tol_eq, tol_ineq, tol_comp, qp_tol, qp_mu0;
+    // linearisation cache generation: bumped by every host call that changes what the
+    // linearisation depends on (iterate, GPs, model parameters, GP switch); 0 disables the cache
+    int32_t lin_gen;
     GPDev gp[kMaxGP];
 };
 
@@ -86,6 +89,13 @@ struct StateDev {
     int32_t* has_prev;   // [B] previous solution valid -> tighten (gpmpc.py:432-433)
     const double* var;   // [B][H][n_gp] GP variances at the previous solution (incl. noise)
     double* tight;       // [B][H+1][2*nb] tightening values (state lo|hi, input lo|hi), optional
+    // Linearisation of the stored iterate (x, u above): [B][H][nx][nb+1], per stage the rows of
+    // [A_k B_k | F_k] with F_k = RK4(x_k, u_k), written by the step that produced the iterate.
+    // The next step's first SQP iteration linearises at exactly that iterate (acados keeps it as
+    // the initial guess), so it reads the rows instead of recomputing them when lin_tag[b] equals
+    // ProblemDev::lin_gen.  Optional (NULL: always recompute).
+    double* lin;
+    int32_t* lin_tag;    // [B]
 };
 
 struct StepIO {

@@ -3185,6 +3185,21 @@ struct SqpKernel {
             v0 = (e == e && v0 == v0) ? fmax(v0, e) : __builtin_nan("");
         }
         const bool x0_ok = v0 <= P.tol_ineq;   // uniform: x0 and the bounds are the same on every lane
+        // linearisation cache: the rows of the stored iterate's linearisation (StateDev::lin) are
+        // valid when the step that stored the iterate also stored them and no host call since has
+        // changed the iterate, the GPs or the model (lin_tag == lin_gen)
+        double* lin_b = S.lin ? S.lin + (size_t)b * H * NX * GS : nullptr;
+        const bool lin_hit = lin_b != nullptr && P.lin_gen != 0 &&
+                             __builtin_amdgcn_readfirstlane(S.lin_tag[b]) == P.lin_gen;
+        // store this step's final linearisation (and F of this lane's stage) before a good exit
+        auto lin_store = [&](const double (&Fs)[NX]) {
+            if (lin_b == nullptr) return;
+            for (int e = lane; e < H * NX * GS; e += 64) lin_b[e] = L.G[e];
+            if (lane < H) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) lin_b[(size_t)lane * NX * GS + i * GS + NB] = Fs[i];
+            }
+        };
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
         int status = kMaxIter, it = 0, qp_total = 0;
         double res[4] = {0, 0, 0, 0};
@@ -3206,7 +3221,14 @@ struct SqpKernel {
 #else
             unsigned long long* tgp = nullptr;
 #endif
-            linearize(P, L, H, lane, w, F, tgp);
+            if (it == 0 && lin_hit) {
+                // the first SQP iteration linearises at the stored iterate: identical rows
+                for (int e = lane; e < H * NX * GS; e += 64) L.G[e] = lin_b[e];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) F[i] = (lane < H) ? lin_b[(size_t)lane * NX * GS + i * GS + NB] : 0.0;
+            } else {
+                linearize(P, L, H, lane, w, F, tgp);
+            }
             WSYNC();
             TPHASE(2);
             // stage reference (gpmpc.py:356-361)
@@ -3255,9 +3277,10 @@ struct SqpKernel {
             if (!(res[0] == res[0] && res[1] == res[1] && res[2] == res[2] && res[3] == res[3])) { status = kNaN; break; }
             if (res[0] <= P.tol_stat && res[1] <= P.tol_eq && res[2] <= P.tol_ineq && res[3] <= P.tol_comp) {
                 status = kSuccess;
+                lin_store(F);
                 break;
             }
-            if (it == P.max_iter) { status = kMaxIter; break; }
+            if (it == P.max_iter) { status = kMaxIter; lin_store(F); break; }
 
             // ---------------- QP in the step variables (HPIPM's role): qp_ipm
             // qv(): variable vb + j of stage kq from a stage vector held in the lane = stage layout.
@@ -3402,6 +3425,7 @@ struct SqpKernel {
 #pragma unroll
             for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
             S.has_prev[b] = good ? 1 : 0;
+            if (lin_b != nullptr) S.lin_tag[b] = good ? P.lin_gen : 0;
             if (io.stats != nullptr) {
                 long long* st = io.stats + (size_t)b * kStatsSlots;
                 st[0] += it;

@@ -147,3 +147,55 @@ def test_mpc_q_r_weights_change_the_solution():
         assert st == 0
         assert np.abs(u[name] - orc.u[0]).max() <= 1e-4 * (1 + np.abs(orc.u).max()), (name, u[name], orc.u[0])
     assert np.abs(u["default"] - u["custom"]).max() > 1e-3
+
+
+@pytest.mark.parametrize("model,H,n", [("quad2d", 30, 200), ("quad3d", 15, 60)])
+def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
+    """The first SQP iteration of a step reads the stored iterate's linearisation (written by the
+    step that produced the iterate) instead of recomputing it.  Against a solver with the cache off
+    (GPMPC_LIN_CACHE=0) every output is bit-identical over a closed loop that also re-uploads the
+    GPs, resets the iterate and sets it from outside (each of which must invalidate the cache)."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(model, n)
+    _, data2, hyp2 = problem(model, n, seed=2)
+    B = 16
+    mats = lqr(spec)
+
+    def make():
+        s = BatchSolver(spec, H, B)
+        s.set_gps(product_gps(data, hyp))
+        s.set_tightening(True, 0.95, *mats)
+        s.reset(reset_iterate=True)
+        return s
+
+    on = make()
+    monkeypatch.setenv("GPMPC_LIN_CACHE", "0")
+    off = make()
+    monkeypatch.delenv("GPMPC_LIN_CACHE")
+    traj = spec.reference_trajectory()
+    x0, ph = initial_states(spec, traj, B)
+    x = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    for k in range(9):
+        if k == 3:
+            for s in (on, off):   # new GPs (GPMPC.reset after train_gp)
+                s.set_gps(product_gps(data2, hyp2))
+                s.reset(reset_iterate=True)
+        if k == 5:
+            xi, ui, _ = on.solution()
+            for s in (on, off):
+                s.set_iterate(xi * 0.5, ui)
+        if k == 7:
+            for s in (on, off):
+                s.reset(reset_iterate=False)
+        outs = []
+        for s in (on, off):
+            u = s.solve(x, ts + k).clone()
+            outs.append((u, s.status.clone(), s.sqp_iter.clone(), s.qp_iter.clone(), s.res.clone(), *s.solution()[:2]))
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), k
+        if model == "quad2d":
+            assert (outs[0][1] == 0).all(), outs[0][1]
+        x = on.plant_step(x, outs[0][0])
