@@ -296,7 +296,7 @@ def run_gpu(args, rank, local_rank, world):
     elapsed, sqp_sum, var_sum = reduce_timing(dist, elapsed, [sum(sqp_list), sum(var_list)], dev)
     tot = stats_buf.sum(0).to(torch.float64)
     mx = stats_buf.max(0).values.to(torch.float64)
-    sums, status_counts, maxes = tot[:2].clone(), tot[2:7].clone(), mx[7:9].clone()
+    sums, status_counts, maxes = torch.cat([tot[:2], tot[9:10]]), tot[2:7].clone(), mx[7:9].clone()
     if dist is not None:
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
@@ -304,17 +304,19 @@ def run_gpu(args, rank, local_rank, world):
     total_instances = B * world
     value = total_instances * args.steps / elapsed
     sqp_mean = float(sums[0]) / (total_instances * args.steps)
+    lin_mean = float(sums[2]) / (total_instances * args.steps)   # linearisations computed per instance-step
     qp_mean = float(sums[1]) / (total_instances * args.steps)
 
     if rank == 0:
         per_lin, exps_lin, var_flops = gp_flops(spec, N, H, getattr(solver, "love_ranks", None))
-        # dominant kernel: the SQP kernel; linearisations per instance-step = sqp_iter + 1
+        # dominant kernel: the SQP kernel; linearisations computed per instance-step = sqp_iter + 1,
+        # minus the one read from the linearisation cache (lin_mean, counted by the kernel)
         sqp_ms = sqp_sum / max(len(sqp_list), 1)
-        flops_sqp = B * (sqp_mean + 1.0) * per_lin          # per launch (one rank's batch)
+        flops_sqp = B * lin_mean * per_lin          # per launch (one rank's batch)
         achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
         var_ms = var_sum / max(len(var_list), 1)
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if var_list else None
-        exps_launch = B * (sqp_mean + 1.0) * exps_lin
+        exps_launch = B * lin_mean * exps_lin
         workload = workload_name(spec, args)
         traffic, traffic_src = None, None
         try:
@@ -375,6 +377,7 @@ def run_gpu(args, rank, local_rank, world):
                 "max": float(sq.max()), "per_step": [round(float(v), 4) for v in sq]},
             "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
             "sqp_iter_mean": sqp_mean,
+            "linearisations_per_step": lin_mean,
             "sqp_iter_max": int(maxes[0]),
             "qp_iter_mean_per_step": qp_mean,
             "qp_iter_max_per_step": int(maxes[1]),

@@ -108,7 +108,8 @@ struct StepIO {
     double* res;             // [B][4] out, final NLP residuals (stat, eq, ineq, comp)
     unsigned long long* timing;  // [B][kPhases] phase cycles (GPMPC_TIMING builds only), may be null
     long long* stats;            // [B][kStatsSlots] sqp iters, qp iters (sums), status 0..4 counts,
-                                 // max sqp iters, max qp iters per solve; may be null
+                                 // max sqp iters, max qp iters per solve, linearisations
+                                 // computed; may be null
 };
 
 // Arguments of the GP posterior kernel (gp_kernels.hip).

@@ -3433,6 +3433,7 @@ struct SqpKernel {
                 if (status >= 0 && status <= 4) st[2 + status] += 1;
                 st[7] = max(st[7], (long long)it);
                 st[8] = max(st[8], (long long)qp_total);
+                st[9] += x0_ok ? it + 1 - (lin_hit ? 1 : 0) : 0;   // linearisations computed
             }
         }
     }

@@ -182,7 +182,9 @@ gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
 /* Optional device buffer [max_batch][10] (int64) of running solver statistics, accumulated by the
  * SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
  * of solves that ended with status s (0..4), [7] largest SQP iteration count of one solve,
- * [8] largest QP iteration total of one solve, [9] reserved.  The caller zeroes it; NULL
+ * [8] largest QP iteration total of one solve, [9] linearisations computed (the first SQP
+ * iteration of a step reads the stored iterate's linearisation when it is valid).  The caller
+ * zeroes it; NULL
  * disables (default).
  * Replaces reading acados' per-solve "sqp_iter" / "qp_iter" / status stats in a host loop. */
 gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev);
