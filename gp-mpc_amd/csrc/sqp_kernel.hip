@@ -3192,13 +3192,16 @@ struct SqpKernel {
         const bool lin_hit = lin_b != nullptr && P.lin_gen != 0 &&
                              __builtin_amdgcn_readfirstlane(S.lin_tag[b]) == P.lin_gen;
         // store this step's final linearisation (and F of this lane's stage) before a good exit
+        // (F goes into the c column of G' first, dead at this point, so the rows leave in one
+        // coalesced pass)
         auto lin_store = [&](const double (&Fs)[NX]) {
             if (lin_b == nullptr) return;
-            for (int e = lane; e < H * NX * GS; e += 64) lin_b[e] = L.G[e];
             if (lane < H) {
 #pragma unroll
-                for (int i = 0; i < NX; ++i) lin_b[(size_t)lane * NX * GS + i * GS + NB] = Fs[i];
+                for (int i = 0; i < NX; ++i) L.G[(size_t)lane * NX * GS + i * GS + NB] = Fs[i];
             }
+            WSYNC();
+            for (int e = lane; e < H * NX * GS; e += 64) lin_b[e] = L.G[e];
         };
         // ---------------- SQP-GN, full steps (gpmpc.py:257-264, 364)
         int status = kMaxIter, it = 0, qp_total = 0;

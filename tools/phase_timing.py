@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--no-gp", action="store_true", help="nominal dynamics (isolates the GP sums)")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference")
+    ap.add_argument("--dump", default="", help="save the per-step per-instance phase cycles (.npy)")
     args = ap.parse_args()
     from gpmpc import _lib
     from gpmpc.gp import GaussianProcess
@@ -81,16 +82,20 @@ def main():
         s.plant_step(obs, u0, ts, out=obs)
     tot = np.zeros(len(PHASES))
     crit = np.zeros(len(PHASES))   # the slowest instance of each step (it sets the kernel time)
+    per_step = []
     s.set_profiling(True)
     s.kernel_times()
     for _ in range(args.steps):
         u0 = s.solve(obs, ts)
         torch.cuda.synchronize()
         tb = tbuf.cpu().numpy().astype(np.float64)
+        per_step.append(tb.copy())
         tot += tb.mean(0)
         crit += tb[np.argmax(tb[:, :-1].sum(1))]
         s.plant_step(obs, u0, ts, out=obs)
     kt = s.kernel_times()
+    if args.dump:
+        np.save(args.dump, np.stack(per_step))
     cyc = tot / args.steps
     sub = cyc[-1]            # GP sums: a sub-phase of "linearize", not part of the total
     cyc = cyc[:-1]
