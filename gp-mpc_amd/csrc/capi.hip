@@ -81,6 +81,8 @@ struct gpmpc_handle {
     // optional per-kernel HIP-event timing (bench.py's roofline leg)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
+    // (start, end) per launch; a variance launch's end event is also the following SQP launch's
+    // start (one event between the two kernels), so the SQP list owns it
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_var, ev_sqp;
     unsigned long long* timing = nullptr;  // diagnostic phase cycles (GPMPC_TIMING builds)
     long long* stats = nullptr;            // optional per-instance solver statistics accumulators
@@ -95,7 +97,11 @@ static hipEvent_t take_event(gpmpc_handle* h) {
         return e;
     }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    // timing-only events: no system-scope fence (cache writeback / invalidate) when recorded,
+    // which otherwise adds ~5 us of dispatch gap around every kernel it brackets
+    const char* ev = std::getenv("GPMPC_EVENT_FENCE");   // "1": default (fenced) events, for A/B
+    const unsigned flags = (ev && ev[0] == '1') ? hipEventDefault : hipEventDisableSystemFence;
+    if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -108,8 +114,8 @@ static void bump_lin(gpmpc_handle* h) {
 static void free_handle(gpmpc_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
-    for (auto* v : {&h->ev_var, &h->ev_sqp})
-        for (auto& pr : *v) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
+    for (auto& pr : h->ev_var) h->ev_pool.push_back(pr.first);
+    for (auto& pr : h->ev_sqp) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain, h->lin})
         if (p) (void)hipFree(p);
@@ -513,7 +519,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     ProblemDev P = h->P;
     P.tighten = (h->P.tighten && h->P.use_gp) ? 1 : 0;
     // 1. GP variances at the previous solution (the MFMA contraction), only when needed
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, mid = nullptr;
     if (P.tighten && h->any_prev) {
         if (h->profiling) {
             e0 = take_event(h);
@@ -548,6 +554,10 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         if (e0 && e1) {
             HIPCHK(hipEventRecord(e1, s));
             h->ev_var.push_back({e0, e1});
+            mid = e1;   // also the SQP launch's start
+        } else {
+            if (e0) h->ev_pool.push_back(e0);
+            if (e1) h->ev_pool.push_back(e1);
         }
     }
     // 2. the SQP step
@@ -559,14 +569,19 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     if (!io.res) io.res = h->scratch_d;
     e0 = e1 = nullptr;
     if (h->profiling) {
-        e0 = take_event(h);
+        e0 = mid;
+        if (!e0) {
+            e0 = take_event(h);
+            if (e0) HIPCHK(hipEventRecord(e0, s));
+        }
         e1 = take_event(h);
-        if (e0) HIPCHK(hipEventRecord(e0, s));
     }
     HIPCHK(launch_sqp(P, S, io, batch, s));
     if (e0 && e1) {
         HIPCHK(hipEventRecord(e1, s));
         h->ev_sqp.push_back({e0, e1});
+    } else if (e0 && !mid) {
+        h->ev_pool.push_back(e0);
     }
     h->any_prev = true;
     return GPMPC_OK;
@@ -581,7 +596,9 @@ gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled) {
 gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     (void)hipSetDevice(h->device);
+    // (the variance list's end events belong to the SQP list, which returns them to the pool)
     auto sum = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
+        const bool owns_end = &v == &h->ev_sqp;
         double acc = 0.0;
         for (auto& pr : v) {
             HIPCHK(hipEventSynchronize(pr.second));
@@ -589,7 +606,7 @@ gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var,
             HIPCHK(hipEventElapsedTime(&t, pr.first, pr.second));
             acc += t;
             h->ev_pool.push_back(pr.first);
-            h->ev_pool.push_back(pr.second);
+            if (owns_end) h->ev_pool.push_back(pr.second);
         }
         if (ms) *ms = acc;
         if (n) *n = (int32_t)v.size();
@@ -606,7 +623,9 @@ gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     if (cap < 0) return fail(GPMPC_ERR_ARG, "negative capacity");
     (void)hipSetDevice(h->device);
+    // (the variance list's end events belong to the SQP list, which returns them to the pool)
     auto take = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
+        const bool owns_end = &v == &h->ev_sqp;
         int32_t i = 0;
         for (auto& pr : v) {
             HIPCHK(hipEventSynchronize(pr.second));
@@ -615,7 +634,7 @@ gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms
             if (ms && i < cap) ms[i] = t;
             ++i;
             h->ev_pool.push_back(pr.first);
-            h->ev_pool.push_back(pr.second);
+            if (owns_end) h->ev_pool.push_back(pr.second);
         }
         if (n) *n = i;
         v.clear();
