@@ -64,6 +64,12 @@ def gp_flops(spec, n_train, H, love_ranks=None):
     return per_lin, exps_lin, var
 
 
+def survey_flops_per_lin(spec, n_train, H):
+    """SURVEY.md §8(d)'s per-linearisation count as written there: every GP at the 4 RK4 points
+    (the reference's CasADi graph evaluates u-only GPs at each of them too)."""
+    return sum(H * 4 * n_train * (4 * d + 2) for d in spec.gp_dims)
+
+
 def cpu_threads() -> int:
     """Host cores this process may use (the GPU box exports OMP_NUM_THREADS = its CPU share)."""
     env = os.environ.get("OMP_NUM_THREADS")
@@ -355,9 +361,14 @@ def run_gpu(args, rank, local_rank, world):
             "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "note": "FP64 GP mean+gradient contraction flops / HIP-event kernel time; peak = FP64 "
-                                 "dense (vector = matrix on gfx950); the kernel is latency-bound in the "
-                                 "Riccati recursion"},
+                         "note": "FP64 GP mean+gradient contraction flops executed (linearisations computed, "
+                                 "u-only GPs once per stage) / HIP-event kernel time; peak = FP64 dense (vector = "
+                                 "matrix on gfx950); the kernel is latency-bound in the Riccati recursion",
+                         "achieved_survey_8d": B * (sqp_mean + 1.0) * survey_flops_per_lin(spec, N, H)
+                                               / (sqp_ms * 1e-3) / 1e12,
+                         "note_survey_8d": "SURVEY.md 8(d)'s algorithmic count: (sqp_iter + 1) linearisations "
+                                           "per step, every GP at the 4 RK4 points, as the reference computes "
+                                           "them; informational, not the frac above"},
             "roofline_variance": None if var_tf is None else {
                 "kernel": ((f"gp_love_kernel<{max((r + 15) // 16 for r in solver.love_ranks if r)},true> "
                             f"(LOVE root rank {max(r for r in solver.love_ranks if r)})")
