@@ -8,6 +8,8 @@ import subprocess
 import sys
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -38,3 +40,38 @@ def test_self_launch_two_ranks_shards_and_max_timing():
 def test_single_rank_needs_no_launcher():
     out = _run(["--gpus", "1", "--dry-run", "--batch", "4", "--steps", "2", "--warmup", "0"])
     assert out["n_gpus"] == 1 and out["shards"] == [[0, 4, out["shards"][0][2]]]
+
+
+def _gpu_bench(args):
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], capture_output=True, text=True, env=env,
+                       timeout=240, cwd=str(ROOT))
+    if p.returncode != 0 and "no GPU" in p.stderr:
+        pytest.skip("no GPU")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+
+@pytest.mark.gpu
+def test_bench_line_contract_on_the_gpu():
+    """The driver's bench line on a short run: the contract keys, the roofline and
+    cpu_baseline objects, the per-step kernel times and solver statistics are present and
+    consistent (value = instances x steps / time, every instance-step converged)."""
+    out = _gpu_bench(["--gpus", "1", "--steps", "3", "--warmup", "1", "--batch", "64", "--cpu-seconds", "1"])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in out, k
+    assert out["steps"] == 3 and out["n_gpus"] == 1 and out["dtype"] == "f64" and out["scaling"] == "weak"
+    assert abs(out["value"] - 64 * 3 / (out["ms_per_step"] * 3e-3)) <= 1e-6 * out["value"]
+    r = out["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
+    assert 0.0 < r["achieved"] <= r["achieved_survey_8d"]
+    assert len(out["sqp_kernel_ms_per_step_distribution"]["per_step"]) == 3
+    assert out["status_counts"]["0"] == 64 * 3
+    assert 1.0 <= out["linearisations_per_step"] <= out["sqp_iter_mean"] + 1.0
+    cb = out["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
