@@ -75,3 +75,24 @@ def test_bench_line_contract_on_the_gpu():
     assert 1.0 <= out["linearisations_per_step"] <= out["sqp_iter_mean"] + 1.0
     cb = out["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
+
+
+def test_flop_counts_match_survey_8d():
+    """bench.py's roofline flop counts for config 3 (quad2d, N=200, H=30): the executed count
+    evaluates the u-only thrust GP once per stage, SURVEY.md 8(d)'s count at all 4 RK4 points;
+    per linearisation and GP, 2d + 2(d+1) flops per training point and evaluation; the exact
+    variance costs N(N+1) + 2N per stage and GP."""
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
+    import bench
+    from gpmpc.models import get_spec
+
+    spec = get_spec("quad2d")
+    H, N = 30, 200
+    per_lin, exps_lin, var = bench.gp_flops(spec, N, H)
+    thrust, pitch = 2 * 1 + 2 * 2, 2 * 3 + 2 * 4          # d = 1 (T_c) and d = 3 (theta, theta_dot, P_c)
+    assert sorted(spec.gp_dims) == [1, 3]
+    assert per_lin == H * N * (thrust + 4 * pitch) == 372_000
+    assert bench.survey_flops_per_lin(spec, N, H) == H * 4 * N * (thrust + pitch) == 480_000
+    assert exps_lin == H * N * (1 + 4)
+    assert var == 2 * H * (N * (N + 1) + 2 * N)
