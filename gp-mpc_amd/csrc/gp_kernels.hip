@@ -297,8 +297,9 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
 // v_mfma_f64_16x16x4_f64, four K-steps per round with their exps interleaved (exp_rbf_n) and the
 // next round's training rows and root entries loaded a round ahead (the blocks of one GP run
 // together, so its root, 3.6 MB at N = 4000 and 112 columns, streams through L2 once per wave
-// generation).  No 16-tile accumulator array and no LDS: 2-3 waves per SIMD hide the loads, against
-// one barrier per 16-row panel in gp_post_kernel.  sf2 is applied to the squared norm (sf2^2), not
+// generation).  No 16-tile accumulator array and no LDS: the round-ahead loads hide the latency
+// (the two round buffers take 256 VGPRs + 18 AGPRs, one wave per SIMD; two waves per SIMD measured
+// slower), against one barrier per 16-row panel in gp_post_kernel.  sf2 is applied to the squared norm (sf2^2), not
 // to every kernel value.
 constexpr int kLoveWaves = 4;
 template <int NTC, bool FROM_STATE>
