@@ -12,6 +12,8 @@
 
 using namespace gpmpc;
 
+static_assert(GPMPC_STATS_SLOTS == kStatsSlots, "public stats-slot count must match the kernel's");
+
 namespace {
 thread_local std::string g_err;
 
@@ -84,6 +86,9 @@ struct gpmpc_handle {
     // (start, end) per launch; a variance launch's end event is also the following SQP launch's
     // start (one event between the two kernels), so the SQP list owns it
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_var, ev_sqp;
+    // end events of ev_var pairs that no SQP pair took over (the SQP launch failed or got no
+    // end event): the variance list returns these to the pool itself
+    std::vector<hipEvent_t> ev_var_owned;
     unsigned long long* timing = nullptr;  // diagnostic phase cycles (GPMPC_TIMING builds)
     long long* stats = nullptr;            // optional per-instance solver statistics accumulators
     int32_t* scratch_i = nullptr;   // [2][max_batch]
@@ -115,6 +120,7 @@ static void free_handle(gpmpc_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     for (auto& pr : h->ev_var) h->ev_pool.push_back(pr.first);
+    for (hipEvent_t e : h->ev_var_owned) h->ev_pool.push_back(e);
     for (auto& pr : h->ev_sqp) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain, h->lin})
@@ -576,14 +582,32 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         }
         e1 = take_event(h);
     }
-    HIPCHK(launch_sqp(P, S, io, batch, s));
-    if (e0 && e1) {
-        HIPCHK(hipEventRecord(e1, s));
-        h->ev_sqp.push_back({e0, e1});
-    } else if (e0 && !mid) {
-        h->ev_pool.push_back(e0);
+    // events not handed to ev_sqp: the shared `mid` stays in use as ev_var's end event (the
+    // variance list takes ownership of it), the others go back to the pool, on every exit path
+    auto recycle = [&]() {
+        if (e0 && e0 == mid) h->ev_var_owned.push_back(e0);
+        else if (e0) h->ev_pool.push_back(e0);
+        if (e1) h->ev_pool.push_back(e1);
+    };
+    hipError_t le = launch_sqp(P, S, io, batch, s);
+    if (le == hipSuccess && e0 && e1) le = hipEventRecord(e1, s);
+    if (le != hipSuccess) {
+        recycle();
+        return fail(GPMPC_ERR_HIP, std::string("launch_sqp: ") + hipGetErrorString(le));
     }
+    if (e0 && e1) h->ev_sqp.push_back({e0, e1});
+    else recycle();
     h->any_prev = true;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev, void* stream) {
+    if (!h || !var_dev) return fail(GPMPC_ERR_ARG, "null argument");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    (void)hipSetDevice(h->device);
+    const size_t B = batch, H = h->H;
+    HIPCHK(hipMemcpyAsync(var_dev, h->var, B * H * h->md.ngp * sizeof(double), hipMemcpyDeviceToDevice,
+                          (hipStream_t)stream));
     return GPMPC_OK;
 }
 
@@ -593,12 +617,22 @@ gpmpc_status gpmpc_set_profiling(gpmpc_handle* h, int32_t enabled) {
     return GPMPC_OK;
 }
 
+// true (and forgotten) if `e` is an ev_var end event that the variance list owns
+static bool release_owned(gpmpc_handle* h, hipEvent_t e) {
+    for (size_t i = 0; i < h->ev_var_owned.size(); ++i)
+        if (h->ev_var_owned[i] == e) {
+            h->ev_var_owned.erase(h->ev_var_owned.begin() + i);
+            return true;
+        }
+    return false;
+}
+
 gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var, double* sqp_ms, int32_t* n_sqp) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     (void)hipSetDevice(h->device);
     // (the variance list's end events belong to the SQP list, which returns them to the pool)
     auto sum = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
-        const bool owns_end = &v == &h->ev_sqp;
+        const bool sqp_list = &v == &h->ev_sqp;
         double acc = 0.0;
         for (auto& pr : v) {
             HIPCHK(hipEventSynchronize(pr.second));
@@ -606,7 +640,7 @@ gpmpc_status gpmpc_kernel_times(gpmpc_handle* h, double* var_ms, int32_t* n_var,
             HIPCHK(hipEventElapsedTime(&t, pr.first, pr.second));
             acc += t;
             h->ev_pool.push_back(pr.first);
-            if (owns_end) h->ev_pool.push_back(pr.second);
+            if (sqp_list || release_owned(h, pr.second)) h->ev_pool.push_back(pr.second);
         }
         if (ms) *ms = acc;
         if (n) *n = (int32_t)v.size();
@@ -625,7 +659,7 @@ gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms
     (void)hipSetDevice(h->device);
     // (the variance list's end events belong to the SQP list, which returns them to the pool)
     auto take = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>>& v, double* ms, int32_t* n) -> gpmpc_status {
-        const bool owns_end = &v == &h->ev_sqp;
+        const bool sqp_list = &v == &h->ev_sqp;
         int32_t i = 0;
         for (auto& pr : v) {
             HIPCHK(hipEventSynchronize(pr.second));
@@ -634,7 +668,7 @@ gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms
             if (ms && i < cap) ms[i] = t;
             ++i;
             h->ev_pool.push_back(pr.first);
-            if (owns_end) h->ev_pool.push_back(pr.second);
+            if (sqp_list || release_owned(h, pr.second)) h->ev_pool.push_back(pr.second);
         }
         if (n) *n = i;
         v.clear();
@@ -651,8 +685,13 @@ gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev) {
     return GPMPC_OK;
 }
 
-gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev) {
+gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev, int32_t slots) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (stats_dev && slots < kStatsSlots)
+        return fail(GPMPC_ERR_ARG, "stats buffer needs GPMPC_STATS_SLOTS = " + std::to_string(kStatsSlots) +
+                                       " int64 slots per instance, got " + std::to_string(slots));
+    if (stats_dev && slots != kStatsSlots)
+        return fail(GPMPC_ERR_ARG, "stats buffer row stride must be GPMPC_STATS_SLOTS = " + std::to_string(kStatsSlots));
     h->stats = (long long*)stats_dev;
     return GPMPC_OK;
 }

@@ -12,7 +12,7 @@ constexpr int kMaxNU = 4;
 constexpr int kMaxH = 63;       // one lane per stage 0..H (64-lane wavefront)
 constexpr int kPhases = 12;  // diagnostic phase slots (GPMPC_TIMING builds)
 constexpr int kMaxParams = 16;
-constexpr int kStatsSlots = 10;  // per-instance solver statistics (gpmpc_set_stats_buffer)
+constexpr int kStatsSlots = 10;  // per-instance solver statistics (gpmpc_set_stats_buffer, = GPMPC_STATS_SLOTS)
 
 enum ModelId : int32_t { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };
 

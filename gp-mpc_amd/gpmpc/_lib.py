@@ -47,7 +47,8 @@ SIGNATURES = {
     "gpmpc_kernel_times": (_I, [_P, POINTER(_D), POINTER(_I), POINTER(_D), POINTER(_I)]),
     "gpmpc_kernel_time_list": (_I, [_P, _I, _P, _P, _P, _P]),
     "gpmpc_set_timing_buffer": (_I, [_P, _P]),
-    "gpmpc_set_stats_buffer": (_I, [_P, _P]),
+    "gpmpc_set_stats_buffer": (_I, [_P, _P, _I]),
+    "gpmpc_get_variance": (_I, [_P, _I, _P, _P]),
     "gpmpc_lds_bytes": (c_int64, [_I, _I]),
 }
 

@@ -183,7 +183,7 @@ class BatchSolver:
         if buf is not None:
             assert buf.shape == (self.batch, self.STATS_SLOTS) and buf.dtype == torch.int64 and buf.device == self.device
         self._stats = buf
-        _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr()))
+        _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr(), self.STATS_SLOTS))
 
     def set_profiling(self, enabled: bool):
         _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))
@@ -237,6 +237,13 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_get_solution(self._h, self.batch, x.data_ptr(), u.data_ptr(), t.data_ptr(),
                                                self._stream()))
         return x, u, t
+
+    def variance(self) -> torch.Tensor:
+        """GP variances (B, H, n_gp) the last tightening used (gpmpc_get_variance): the variance
+        kernel's output at the previous solution, likelihood noise included."""
+        v = torch.empty(self.batch, self.H, self.spec.n_gp, dtype=torch.float64, device=self.device)
+        _lib.check(self.lib.gpmpc_get_variance(self._h, self.batch, v.data_ptr(), self._stream()))
+        return v
 
     def plant_step(self, x: torch.Tensor, u: torch.Tensor, tstep: torch.Tensor | None = None,
                    params: dict | None = None, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -137,6 +137,11 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
 gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, double* u_dev, double* tight_dev,
                                 void* stream);
 
+/* Copy the GP variances the last tightening used (the variance kernel's output at the previous
+ * solution, likelihood noise included, gpmpc/gpmpc.py:437-445) into var [B][H][n_gp] (device).
+ * Diagnostic / parity surface: the values the constraint tightening consumed. */
+gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev, void* stream);
+
 /* GP posterior at P points Z [P][d] (device): mean [P] and/or variance [P] (either may be
  * NULL; variance needs Linv).  with_noise = 1 adds the likelihood noise
  * (gp.likelihood(gp(z)), gpmpc/gpmpc.py:444).  GaussianProcess.predict() of the build. */
@@ -179,15 +184,17 @@ gpmpc_status gpmpc_kernel_time_list(gpmpc_handle* h, int32_t cap, double* var_ms
  * per-phase shader-clock cycles of each instance's last solve; NULL disables. */
 gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
 
-/* Optional device buffer [max_batch][10] (int64) of running solver statistics, accumulated by the
- * SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
+/* Optional device buffer [max_batch][GPMPC_STATS_SLOTS] (int64) of running solver statistics,
+ * accumulated by the SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
  * of solves that ended with status s (0..4), [7] largest SQP iteration count of one solve,
  * [8] largest QP iteration total of one solve, [9] linearisations computed (the first SQP
  * iteration of a step reads the stored iterate's linearisation when it is valid).  The caller
- * zeroes it; NULL
- * disables (default).
+ * zeroes it; NULL disables (default).  `slots` is the caller's row stride in int64: it must
+ * equal GPMPC_STATS_SLOTS (a buffer laid out for another slot count is rejected, not
+ * overrun).
  * Replaces reading acados' per-solve "sqp_iter" / "qp_iter" / status stats in a host loop. */
-gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev);
+enum { GPMPC_STATS_SLOTS = 10 };
+gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev, int32_t slots);
 
 /* LDS bytes one instance's workgroup needs (capacity planning / tests). */
 int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon);

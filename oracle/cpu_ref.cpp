@@ -41,6 +41,8 @@ struct GP {
     std::vector<double> X, alpha, L;   // X [n][d], L lower Cholesky of K(Xv, Xv) [nv][nv] (may be empty)
     std::vector<double> Xv;            // variance rows [nv][d]; empty: Xv = X (exact GP).  FITC:
                                        // mean over inducing rows X, variance over the training set
+    std::vector<double> R;             // LOVE root [m][r] of the variance rows (empty: exact variance)
+    int rr = 0;
     double ell = 1, sf2 = 1, sn2 = 0;
     int in_idx[3] = {0, 0, 0}, var_idx[3] = {0, 0, 0};
 
@@ -62,11 +64,26 @@ struct GP {
         for (int k = 0; k < d; ++k) g[k] = gs[k] / (ell * ell);
         return m;
     }
-    // sf2 - |L^-1 k|^2 + sn2  (exact posterior variance with the likelihood noise)
+    // sf2 - |L^-1 k|^2 + sn2  (exact posterior variance with the likelihood noise), or with a LOVE
+    // root R (R R^T ~ K^-1, gpytorch fast_pred_var, gpmpc/gpmpc.py:442-444) sf2 - |R^T k|^2 + sn2
     double var(const double* z, std::vector<double>& v) const {
         const double c = -0.5 / (ell * ell);
         const bool own = !Xv.empty();
         const int m = own ? nv : n;
+        if (rr > 0) {
+            v.assign(rr, 0.0);
+            for (int i = 0; i < m; ++i) {
+                const double* x = own ? &Xv[(size_t)i * d] : &X[(size_t)i * d];
+                double q = 0.0;
+                for (int k = 0; k < d; ++k) q += (x[k] - z[k]) * (x[k] - z[k]);
+                const double s = sf2 * std::exp(c * q);
+                const double* Ri = &R[(size_t)i * rr];
+                for (int j = 0; j < rr; ++j) v[j] += s * Ri[j];
+            }
+            double acc = 0.0;
+            for (int j = 0; j < rr; ++j) acc += v[j] * v[j];
+            return sf2 - acc + sn2;
+        }
         v.resize(m);
         double acc = 0.0;
         for (int i = 0; i < m; ++i) {
@@ -724,6 +741,34 @@ int cpuref_set_gp_var(void* h, int g, int nv, const double* Xv, const double* L)
     G.nv = nv;
     G.Xv.assign(Xv, Xv + (size_t)nv * G.d);
     G.L.assign(L, L + (size_t)nv * nv);
+    return 0;
+}
+
+// LOVE variance of GP g: R [m][r] row-major over the variance rows (m = nv, or n for an exact GP),
+// R R^T ~ (K + sn2 I)^-1 (gpmpc/gp.py love_root); R = NULL restores the exact variance.
+int cpuref_set_gp_var_root(void* h, int g, int m, int r, const double* R) {
+    Problem& P = static_cast<Handle*>(h)->P;
+    if (g < 0 || g >= P.ngp) return -1;
+    GP& G = P.gp[g];
+    if (!R) {
+        G.R.clear();
+        G.rr = 0;
+        return 0;
+    }
+    if (m != (G.Xv.empty() ? G.n : G.nv) || r < 1) return -1;
+    G.R.assign(R, R + (size_t)m * r);
+    G.rr = r;
+    return 0;
+}
+
+// Tightening variance of GP g (likelihood noise included) at P points Z [P][d] -> out [P].
+int cpuref_gp_var(void* h, int g, int P, const double* Z, double* out) {
+    const Problem& Pr = static_cast<Handle*>(h)->P;
+    if (g < 0 || g >= Pr.ngp || P < 0) return -1;
+    const GP& G = Pr.gp[g];
+    if (G.L.empty() && G.rr == 0) return -1;
+    std::vector<double> v;
+    for (int p = 0; p < P; ++p) out[p] = G.var(Z + (size_t)p * G.d, v);
     return 0;
 }
 

@@ -19,6 +19,8 @@ _SIGS = {
     "cpuref_set_options": (None, [_P, _I, _D, _I, _D]),
     "cpuref_set_gp": (_I, [_P, _I, _I, _I, _P, _P, _P, _D, _D, _D, _P, _P]),
     "cpuref_set_gp_var": (_I, [_P, _I, _I, _P, _P]),
+    "cpuref_set_gp_var_root": (_I, [_P, _I, _I, _I, _P]),
+    "cpuref_gp_var": (_I, [_P, _I, _I, _P, _P]),
     "cpuref_use_gp": (None, [_P, _I]),
     "cpuref_set_tightening": (None, [_P, _I, _D, _P, _P, _P, _P, _I]),
     "cpuref_set_reference": (None, [_P, _P, _I]),
@@ -48,9 +50,12 @@ class CpuRef:
     """B instances of the control step on the host (GPMPC.select_action semantics, batched)."""
 
     def __init__(self, spec, H: int, B: int, gps=None, lqr_mats=None, prob: float = 0.95, uh: float = -1e-8,
-                 tol: float = 1e-6, qp_tol: float = 1e-8, qp_max_iter: int = 50, max_iter: int = 25, fitc=None):
+                 tol: float = 1e-6, qp_tol: float = 1e-8, qp_max_iter: int = 50, max_iter: int = 25, fitc=None,
+                 love_roots=None):
         """``fitc[g] = (S (M, d), w (M,))``: GP g's mean over the inducing rows S with weights w
-        (`gpmpc/gpmpc.py:175-187,377-400`); its variance stays the exact GP's (``gps[g]``)."""
+        (`gpmpc/gpmpc.py:175-187,377-400`); its variance stays the exact GP's (``gps[g]``).
+        ``love_roots[g]`` (n, r) or None: GP g's tightening variance from that LOVE root (the
+        reference's ``fast_pred_var``, `gpmpc/gpmpc.py:442-444`) instead of the exact L^-1 k."""
         from oracle import gpmpc_oracle as O
 
         self.lib = load()
@@ -83,6 +88,10 @@ class CpuRef:
                 else:
                     rc = self.lib.cpuref_set_gp(self.h, g, X.shape[0], X.shape[1], X.ctypes.data, a.ctypes.data,
                                                 L.ctypes.data, gp.ell, gp.sf2, gp.sn2, ii.ctypes.data, vi.ctypes.data)
+                if rc == 0 and love_roots is not None and love_roots[g] is not None:
+                    R = _c(love_roots[g])
+                    self._keep.append(R)
+                    rc = self.lib.cpuref_set_gp_var_root(self.h, g, R.shape[0], R.shape[1], R.ctypes.data)
                 if rc != 0:
                     raise RuntimeError(f"cpuref_set_gp({g}) failed")
             self.lib.cpuref_use_gp(self.h, 1)
@@ -103,6 +112,14 @@ class CpuRef:
         self.status = np.zeros(B, np.int32)
         self.sqp_iter = np.zeros(B, np.int32)
         self.qp_iter = np.zeros(B, np.int32)
+
+    def gp_var(self, g: int, Z: np.ndarray) -> np.ndarray:
+        """GP g's tightening variance (noise included) at Z (P, d): exact or from its LOVE root."""
+        Z = _c(Z)
+        out = np.zeros(Z.shape[0])
+        if self.lib.cpuref_gp_var(self.h, g, Z.shape[0], Z.ctypes.data, out.ctypes.data) != 0:
+            raise RuntimeError(f"cpuref_gp_var({g}) failed")
+        return out
 
     def step(self, x0: np.ndarray, tstep: np.ndarray, threads: int = 1) -> np.ndarray:
         x0 = _c(x0)

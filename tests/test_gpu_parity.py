@@ -98,11 +98,13 @@ def test_gp_predict_edge_cases():
                                                       ("quad3d", 120, 40, 1, 2, 60, False),
                                                       ("quad2d", 1000, 30, 2, 2, None, False),
                                                       ("quad2d", 200, 30, 3, 3, None, True),
-                                                      ("quad3d", 120, 40, 1, 2, 60, True)])
+                                                      ("quad3d", 120, 40, 1, 2, 60, True),
+                                                      ("quad2d", 1000, 30, 4, 2, None, "default")])
 def test_closed_loop_parity(name, N, H, B, steps, M, love):
     """M: FITC mean on M inducing rows (`gpmpc/gpmpc.py:377-400`, config 5's sparse GP), exact variance.
     love: the tightening variance from the LOVE root (gpytorch fast_pred_var, `gpmpc/gpmpc.py:442-444`;
-    forced at every size here), the oracle's variance from the same root (oracle.love_var)."""
+    True: forced at every size; "default": the solver's default, LOVE above 800 training rows, i.e.
+    config 4's N=1000), the oracle's variance from the same root (oracle.love_var)."""
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
@@ -114,12 +116,16 @@ def test_closed_loop_parity(name, N, H, B, steps, M, love):
         gpo = fitc_oracle_gps(gpo, fitc)
     if love:
         for og, gp in zip(gpo, gpp):
+            if love == "default" and N <= 800:
+                continue
             R = gp.love_root(100).cpu().numpy()
             og.var = (lambda Z, with_noise=True, og=og, R=R: O.love_var(og, R, Z, with_noise))
     mats = lqr(spec)
     tol = 1e-9
     solver = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)  # tight KKT for parity
-    solver.set_gps(gpp, fitc=fitc, variance="love" if love else "exact", love_force=love)
+    solver.set_gps(gpp, fitc=fitc, variance="love" if love else "exact", love_force=love is True)
+    if love == "default":
+        assert all(r is not None for r in solver.love_ranks), solver.love_ranks
     solver.set_tightening(True, 0.95, *mats)
     solver.reset(reset_iterate=True)
     sd = spec.to_dict()
