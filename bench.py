@@ -78,46 +78,66 @@ def cpu_threads() -> int:
     return len(os.sched_getaffinity(0))
 
 
-def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, fitc=None, heavy=False):
+def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, x0_all, phase_all, ids, warmup, steps, fitc=None,
+                 love_roots=None):
     """Time the C++ CPU restatement (oracle/cpu_ref.cpp: SQP-GN + Mehrotra IPM with Riccati
-    Newton steps, OpenMP over instances) on a bounded closed-loop sample of the same workload:
-    all host cores over a batch of instances (value; 4 per thread, 1 per thread for heavy
-    workloads), and one instance on one core (the reference's usage pattern).  The first, cold
-    step of each run is not timed (gpmpc/plotting.py:25)."""
+    Newton steps, OpenMP over instances, the same tightening variance as the GPU leg: exact or
+    the same LOVE roots) on the GPU leg's own window: the same global instance ids (an evenly
+    spaced sample of them when the whole shard does not fit the CPU budget), the same initial
+    states and reference phases, closed-loop steps 0 .. warmup-1 untimed and steps
+    warmup .. warmup+steps-1 timed, as the GPU leg (the first, cold step is never timed,
+    gpmpc/plotting.py:25).  All host cores over the sample (value), and a sub-sample with one
+    instance at a time on one core (the reference's usage pattern)."""
     from oracle import cpu_ref
     from oracle import gpmpc_oracle as O
-    from gpmpc.synthetic import initial_states
 
     gps = [O.ExactGP(X, y, *hyp[i]) for i, (X, y) in enumerate(data)]
     plant = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
-    traj = spec.reference_trajectory()
-
-    def run(B, threads, budget):
-        ref = cpu_ref.CpuRef(spec, H, B, gps=gps, lqr_mats=lqr_mats, fitc=fitc)
-        x0, phase = initial_states(spec, traj, B)
-        steps, elapsed, k = 0, 0.0, 0
-        while elapsed < budget or steps < 1:
-            t0 = time.perf_counter()
-            u0 = ref.step(x0, phase + k, threads=threads)
-            dt = time.perf_counter() - t0
-            if k > 0:
-                steps += 1
-                elapsed += dt
-            for b in range(B):
-                x0[b] = plant.rk4(x0[b], u0[b])[0]
-            k += 1
-        return B * steps / elapsed, steps, ref
-
+    ids = np.asarray(ids)
     threads = cpu_threads()
-    Bc = (1 if heavy else 4) * threads
-    v_all, n_all, ref = run(Bc, threads, 0.65 * seconds)
-    v_one, n_one, _ = run(1, 1, 0.35 * seconds)
-    return {"value": float(v_all), "unit": "control steps/s", "cores": threads, "kind": "port",
-            "single_instance_1core": float(v_one),
+    window = warmup + steps
+
+    def run(sel, nthreads):
+        ref = cpu_ref.CpuRef(spec, H, len(sel), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots)
+        x0 = x0_all[sel].copy()
+        phase = phase_all[sel].astype(np.int32)
+        elapsed, sqp = 0.0, 0
+        for k in range(window):
+            t0 = time.perf_counter()
+            u0 = ref.step(x0, phase + k, threads=nthreads)
+            dt = time.perf_counter() - t0
+            if k >= warmup:
+                elapsed += dt
+                sqp += int(ref.sqp_iter.sum())
+            for b in range(len(sel)):
+                x0[b] = plant.rk4(x0[b], u0[b])[0]
+        return elapsed, sqp
+
+    # per-instance-step cost from one cold step of `threads` instances (an upper bound: the cold
+    # step needs the most SQP iterations), then the largest sample the budget allows
+    probe = ids[np.linspace(0, len(ids) - 1, min(threads, len(ids))).astype(int)]
+    ref = cpu_ref.CpuRef(spec, H, len(probe), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots)
+    t0 = time.perf_counter()
+    ref.step(x0_all[probe].copy(), phase_all[probe].astype(np.int32), threads=threads)
+    t_inst = (time.perf_counter() - t0) * threads / len(probe)     # core-seconds per instance-step
+    n_all = int(0.65 * seconds * threads / (window * t_inst))
+    n_all = max(min(threads, len(ids)), min(len(ids), n_all // threads * threads if n_all >= threads else n_all))
+    sel = ids[np.linspace(0, len(ids) - 1, n_all).astype(int)] if n_all < len(ids) else ids
+    el_all, sqp_all = run(sel, threads)
+    n_one = max(1, min(len(sel), 64, int(0.35 * seconds / (window * t_inst))))
+    sel1 = sel[np.linspace(0, len(sel) - 1, n_one).astype(int)]
+    el_one, _ = run(sel1, 1)
+    var = ("LOVE roots of ranks " + "/".join(str(None if R is None else R.shape[1]) for R in love_roots)
+           if love_roots is not None and any(R is not None for R in love_roots) else "exact variance")
+    return {"value": float(len(sel) * steps / el_all), "unit": "control steps/s", "cores": threads, "kind": "port",
+            "single_instance_1core": float(len(sel1) * steps / el_one),
+            "sqp_iter_mean": sqp_all / (len(sel) * steps),
+            "instances": int(len(sel)), "window": [int(warmup), int(warmup + steps)],
             "sample": f"C++ restatement (oracle/cpu_ref.cpp, -O3 AVX2, OpenMP), {spec.name} N={data[0][0].shape[0]}"
-                      f"{' FITC M=%d' % len(fitc[0][1]) if fitc else ''} H={H}: {Bc} instances x {n_all} closed-loop "
-                      f"steps on {threads} threads; single_instance_1core: 1 instance x {n_one} steps on 1 thread; "
-                      f"first step of each run untimed; sqp_iter mean {float(ref.sqp_iter.mean()):.2f}"}
+                      f"{' FITC M=%d' % len(fitc[0][1]) if fitc else ''} H={H}, {var}: {len(sel)} of the GPU leg's "
+                      f"{len(ids)} instances (same ids, initial states and reference phases), closed-loop steps "
+                      f"{warmup}..{warmup + steps - 1} timed after {warmup} untimed, on {threads} threads; "
+                      f"single_instance_1core: {len(sel1)} of them one at a time on 1 thread over the same steps"}
 
 
 def parse_args(argv=None):
@@ -125,7 +145,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="total instances over all GPUs, contiguous B/G slices per rank (strong scaling, "
+                         "SURVEY.md 8(e)); overrides --batch")
     ap.add_argument("--model", default="quad2d")
     ap.add_argument("--n-train", type=int, default=200)
     ap.add_argument("--horizon", type=int, default=30)
@@ -147,13 +170,14 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def workload_name(spec, args):
+def workload_name(spec, args, world=1):
     N, H, B = args.n_train, args.horizon, args.batch
+    per = f"{B} instances per GPU" if not args.global_batch else f"global batch {args.global_batch} over {world} GPU(s)"
     return (f"{spec.name} GP-MPC N={N}{' FITC M=%d' % min(args.fitc, N) if args.fitc else ''} H={H}"
             f"{', variance at the GP inputs' if args.var_inputs == 'dynamics' else ''}"
             f"{', LOVE variance' if getattr(args, 'variance', 'exact') == 'love' and N > 800 else ''}"
             f"{', exact variance' if getattr(args, 'variance', 'exact') == 'exact' and N > 800 else ''}, "
-            f"{B} instances per GPU, closed loop")
+            f"{per}, closed loop")
 
 
 def init_dist(world, gpu, use_gpu):
@@ -189,7 +213,7 @@ def run_dry(args, rank, world):
 
     dist = init_dist(world, 0, use_gpu=False)
     spec = get_spec(args.model)
-    ids = D.shard_range(args.batch, rank)
+    ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
     for _ in range(args.warmup):
         time.sleep(1e-3 * (1 + rank))
     if dist is not None:
@@ -208,12 +232,13 @@ def run_dry(args, rank, world):
     else:
         shards = [[ids.start, ids.stop, local]]
     if rank == 0:
-        total = args.batch * world
+        total = args.global_batch or args.batch * world
         print(json.dumps({"metric": METRIC, "value": total * args.steps / elapsed, "unit": "control steps/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                          "scaling": "strong" if args.global_batch else "weak",
                           "vs_baseline": None, "dtype": "f64", "data": "dry run (host sleep, no GPU)",
-                          "config": {"workload": workload_name(spec, args), "model": spec.name,
+                          "config": {"workload": workload_name(spec, args, world), "model": spec.name,
                                      "global_batch": total, "horizon": args.horizon, "n_train": args.n_train,
                                      "parallelism": f"instances sharded over {world} rank(s)"},
                           "shards": shards}))
@@ -241,7 +266,12 @@ def run_gpu(args, rank, local_rank, world):
     spec = get_spec(args.model)
     if args.var_inputs == "dynamics":
         spec.var_inputs = spec.gp_inputs
-    H, B, N = args.horizon, args.batch, args.n_train
+    H, N = args.horizon, args.n_train
+    # instances of this rank: contiguous global ids (weak: rank*B .. rank*B+B-1; strong: the rank's
+    # slice of the global batch), no collective in the data path
+    ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
+    B = len(ids)
+    total_instances = args.global_batch or args.batch * world
     data = D.replicate_training_data(make_training_data(spec, N, seed=1), device=dev)  # GP replicated on every rank
     hyp = DEFAULT_HYPERS[spec.name]
     gps = []
@@ -267,9 +297,7 @@ def run_gpu(args, rank, local_rank, world):
     solver.set_tightening(True, 0.95, *lqr_mats)
     solver.reset(reset_iterate=True)
     traj = spec.reference_trajectory()
-    # instances of this rank: global ids rank*B .. rank*B+B-1 (contiguous shards, no collective)
-    ids = D.shard_range(B, rank)
-    x0_all, phase_all = initial_states(spec, traj, B * world, seed=1)
+    x0_all, phase_all = initial_states(spec, traj, total_instances, seed=1)
     obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
     tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
     stats_buf = torch.zeros(B, BatchSolver.STATS_SLOTS, dtype=torch.int64, device=dev)   # filled by the SQP kernel
@@ -307,7 +335,6 @@ def run_gpu(args, rank, local_rank, world):
         dist.all_reduce(sums, op=dist.ReduceOp.SUM)
         dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
         dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
-    total_instances = B * world
     value = total_instances * args.steps / elapsed
     sqp_mean = float(sums[0]) / (total_instances * args.steps)
     lin_mean = float(sums[2]) / (total_instances * args.steps)   # linearisations computed per instance-step
@@ -323,7 +350,7 @@ def run_gpu(args, rank, local_rank, world):
         var_ms = var_sum / max(len(var_list), 1)
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if var_list else None
         exps_launch = B * lin_mean * exps_lin
-        workload = workload_name(spec, args)
+        workload = workload_name(spec, args, world)
         traffic, traffic_src = None, None
         try:
             with open(args.pmc_summary) as fh:
@@ -339,8 +366,8 @@ def run_gpu(args, rank, local_rank, world):
             traffic = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
-            heavy = args.fitc > 0 or N >= 2000
-            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, fitc=fitc, heavy=heavy)
+            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, x0_all, phase_all, list(ids),
+                               args.warmup, args.steps, fitc=fitc, love_roots=solver.love_roots)
         sq = np.array(sqp_list) if sqp_list else np.zeros(1)
         out = {
             "metric": METRIC,
@@ -351,13 +378,14 @@ def run_gpu(args, rank, local_rank, world):
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.global_batch else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded GP training set, initial states, figure-eight reference)",
             "config": {"workload": workload,
                        "model": spec.name, "global_batch": total_instances, "horizon": H, "n_train": N,
-                       "parallelism": f"instances sharded over {world} GPU(s), GP replicated"},
+                       "batch_per_gpu": B,
+                       "parallelism": f"instances sharded over {world} GPU(s) in contiguous slices, GP replicated"},
             "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": traffic_src,

@@ -208,6 +208,13 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     {
         const char* ev = std::getenv("GPMPC_LIN_CACHE");   // "0": recompute every linearisation (A/B)
         h->lin_cache = !(ev && ev[0] == '0');
+        const char* ec = std::getenv("GPMPC_CONDENSE");    // "1": condensed stage pairs (A/B)
+        P.condense = (ec && ec[0] == '1') ? 1 : 0;
+        const char* ew = std::getenv("GPMPC_WAVES");       // "1" / "4": waves per instance (A/B)
+        P.waves = ew ? std::atoi(ew) : 0;
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
+        P.n_cu = ncu;
     }
     const size_t lds = sqp_lds_bytes(model_id, horizon);
     if (lds > 160 * 1024) {
@@ -608,6 +615,14 @@ gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev,
     const size_t B = batch, H = h->H;
     HIPCHK(hipMemcpyAsync(var_dev, h->var, B * H * h->md.ngp * sizeof(double), hipMemcpyDeviceToDevice,
                           (hipStream_t)stream));
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves, int32_t condense) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (waves != 0 && waves != 1 && waves != 4) return fail(GPMPC_ERR_ARG, "waves must be 0 (auto), 1 or 4");
+    h->P.waves = waves;
+    h->P.condense = condense ? 1 : 0;
     return GPMPC_OK;
 }
 

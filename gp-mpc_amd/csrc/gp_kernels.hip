@@ -423,7 +423,6 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
         }
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
-#ifndef GPMPC_LOVE_POST
     bool love = true;   // every entry variance-only with a LOVE root of <= 128 columns
     int wmax = 0;
     for (int q = 0; q < pb.n; ++q) {
@@ -433,7 +432,6 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
     }
     if (love)
         return from_state ? launch_love<true>(pb, wmax / 16, stream) : launch_love<false>(pb, wmax / 16, stream);
-#endif
     bool tri = true;   // every entry variance-only with the same npad <= 256
     for (int q = 0; q < pb.n; ++q)
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&

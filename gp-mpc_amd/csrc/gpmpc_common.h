@@ -77,6 +77,11 @@ struct ProblemDev {
     // linearisation cache generation: bumped by every host call that changes what the
     // linearisation depends on (iterate, GPs, model parameters, GP switch); 0 disables the cache
     int32_t lin_gen;
+    // launch shape of the SQP kernel: waves per instance (0: auto -- four when batch <= n_cu for the
+    // single-tile models, sqp_kernel.hip sqp_waves), two-stage condensed recursions (H even)
+    int32_t waves;
+    int32_t condense;
+    int32_t n_cu;             // compute units of the device (set by gpmpc_create)
     GPDev gp[kMaxGP];
 };
 

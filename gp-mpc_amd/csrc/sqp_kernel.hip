@@ -21,6 +21,7 @@
 // obs, u_H absent), its bounds and the dynamics multiplier pi_k.  The IPM state of a stage is
 // split over lanes k and k + 32 when H + 1 <= 32 (SPL).  The Riccati recursion is sequential
 // over stages and parallel over matrix entries.  DESIGN.md §2.1 has the layouts and timings.
+#include <cstdlib>
 #include <type_traits>
 
 #include "gpmpc_common.h"
@@ -97,13 +98,6 @@ __device__ __forceinline__ double xor32_d(double v) {   // value of lane l ^ 32
     const unsigned int rl = up ? lo[0] : lo[1], rh = up ? hi[0] : hi[1];
     return __longlong_as_double(((long long)rh << 32) | rl);
 }
-// Lanes 0..31 receive the value of lane l + 32 (lanes 32..63 are left undefined).
-__device__ __forceinline__ double from_upper_half(double v) {
-    const long long b = __double_as_longlong(v);
-    const auto lo = __builtin_amdgcn_permlane32_swap((int)b, (int)b, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap((int)(b >> 32), (int)(b >> 32), false, false);
-    return __longlong_as_double(((long long)(unsigned int)hi[1] << 32) | (unsigned int)lo[1]);
-}
 // Whole-wave reductions (all 64 lanes active).  Every lane ends with the bitwise-same value:
 // each step combines a lane with a partner holding the mirrored partial (commutative ops).
 template <class Op>
@@ -141,37 +135,11 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 // 1/x to full double precision (no IEEE div sequence): the v_rcp_f64 estimate r0 = (1 - eps)/x,
 // |eps| <= 2^-23, refined by one cubic step r0 (1 + e + e^2), e = 1 - x r0, whose error is eps^3.
 // Three dependent f64 ops after the estimate instead of four for two Newton steps (a dependent
-// f64 VALU op costs ~32 cycles on gfx950, tools/probe_latency.hip).
+// f64 VALU op waits ~7.3 cycles on gfx950, tools/probe_f64.hip).
 __device__ __forceinline__ double fast_rcp(double x) {
     const double r = __builtin_amdgcn_rcp(x);
     const double e = fma(-x, r, 1.0);
     return fma(r, fma(e, e, e), r);
-}
-
-// In-register inverse of a small SPD matrix (Gauss-Jordan, no pivoting needed for SPD).
-template <int N>
-__device__ __forceinline__ bool spd_inverse(double (&a)[N][N], double (&inv)[N][N]) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int j = 0; j < N; ++j) inv[i][j] = (i == j) ? 1.0 : 0.0;
-    bool ok = true;
-#pragma unroll
-    for (int c = 0; c < N; ++c) {
-        const double piv = a[c][c];
-        ok = ok && (piv > 0.0);
-        const double r = fast_rcp(piv);
-#pragma unroll
-        for (int j = 0; j < N; ++j) { a[c][j] *= r; inv[c][j] *= r; }
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            if (i == c) continue;
-            const double f = a[i][c];
-#pragma unroll
-            for (int j = 0; j < N; ++j) { a[i][j] -= f * a[c][j]; inv[i][j] -= f * inv[c][j]; }
-        }
-    }
-    return ok;
 }
 
 // GP mean + input gradient at up to 16*NE evaluation points on the f64 matrix cores
@@ -300,7 +268,12 @@ __device__ __attribute__((noinline)) void gp_tiles_dispatch(const double* tX, co
     }
 }
 
+// Waves per instance: the wide model (quad3d) always runs four (its LDS allows one instance per CU);
+// the single-tile models run one, or four when the batch leaves SIMDs idle (launch_sqp_step).
 template <int ID>
+constexpr int kDefaultWaves = (Model<ID>::NB + 1 > 16) ? 4 : 1;
+
+template <int ID, int NW = kDefaultWaves<ID>>
 struct SqpKernel {
     using M = Model<ID>;
     static constexpr int NX = M::NX, NU = M::NU, NB = M::NB, NGP = M::NGP, NUNC = M::NUNC;
@@ -308,34 +281,39 @@ struct SqpKernel {
     static constexpr int PS = NX + 1;   // row stride of P'_k = [P_k | p_k] and K'_k = [K_k | kff_k]
     static constexpr int CB = 4;        // tangent column block
     static constexpr int NCB = (NB + CB - 1) / CB;
-    // entries per Riccati phase and the rounds of 64 lanes they take
-    static constexpr int N1 = NX * GS;                       // W' = P' [G'; e]
-    static constexpr int N2 = GS * (GS + 1) / 2 - 1;         // upper triangle of M' (no corner)
-    static constexpr int N3P = NX * (NX + 1) / 2 + NX;       // P'_k (upper triangle + p column)
-    static constexpr int N3 = N3P + NU * PS;                 // + K'_k
-    static constexpr int R1 = (N1 + 63) / 64, R2 = (N2 + 63) / 64, R3 = (N3 + 63) / 64;
 
     // Riccati on v_mfma_f64_16x16x4 when every stage product fits one 16x16 tile
     // (G' has NB+1 <= 16 columns, the forward state [dx; 1] has NX+1 <= 8 rows).
     static constexpr bool kMfma = (NB + 1 <= 16) && (NX + 1 <= 8);
+    // Two-stage condensing of the Newton systems (kCond, H even): stage pairs (2j, 2j + 1) become
+    // one block with state x_2j and inputs [u_2j; u_2j+1] (NCU <= 4 tile slots), so the sequential
+    // Riccati factorisation and sweeps run over H/2 blocks (cond_backward and the sweeps below).
+    static constexpr int NCU = 2 * NU;
+    static constexpr bool kCond = kMfma && NCU <= 4;
+    // stages per block of the Newton-system recursions for horizon H (1: stage by stage)
+    __host__ __device__ static constexpr int cf_of(int H) { return (kCond && H % 2 == 0) ? 2 : 1; }
+    // multipliers kept in LDS during the step (the layouts with room for them: condensed blocks or
+    // one instance per CU); otherwise they stay in global memory (rows read / written per SQP iteration)
+    __host__ __device__ static constexpr bool lds_mult(int CF) { return NW > 1; }
+    static constexpr int GH = NX + 1 + NCU;   // row of the condensed dynamics G^_j: [G^_x | c^ | G^_u]
     // Waves per instance.  The wide model (quad3d) needs more LDS than two instances per CU can
     // have, so its CU's other SIMDs would idle: three GP helper waves take a share of every GP
-    // tile pass (gp_tiles over tiles w, w + 4, ...), the main wave runs everything else.
-#ifdef GPMPC_W2
-    static constexpr bool kW2 = true;
-#else
-    static constexpr bool kW2 = false;
-#endif
-    // -DGPMPC_W2: two waves per instance for the single-tile models with an even stage width (quad2d)
-    static constexpr int NWAVES = (NB + 1 > 16) ? 4 : ((kW2 && NB % 2 == 0) ? 2 : 1);
+    // tile pass (gp_tiles over tiles w, w + 4, ...) and of the IPM's elementwise work (WSPL), the
+    // main wave runs the recursions.  The single-tile models use the same protocol when the batch
+    // is small enough for every instance to have a CU (B <= CUs): the idle SIMDs then do that work.
+    static constexpr int NWAVES = NW;
+    static_assert(NW == 1 || NW == 4, "one wave per instance or four (one per SIMD of the CU)");
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *W, *Ms, *vs, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
-        double *Dp, *Eb, *XT, *RV;   // cyclic-reduction solver (kCR)
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
         double *Dq, *xs;             // WSPL: step-vector exchange, reduction slots
+        double *Gh, *dpv, *Tc;       // condensed blocks (CF = 2): G^_j rows, dpi of every stage (and
+                                     // the corrector's block gradients), corrector scratch t_j
+        double *lam, *pim;           // the instance's multipliers during the step (acados memory):
+                                     // bounds [H+1][2 NB], dynamics [H][NX]
         int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
@@ -346,87 +324,81 @@ struct SqpKernel {
         // + the helper waves' partial sums [NWAVES-1][16*NE][4]
         return (size_t)9 * NGP * 16 * ((H + 15) / 16) + (size_t)(NWAVES - 1) * 64 * ((H + 15) / 16);
     }
-    __host__ __device__ static size_t p_region(int H) {
-        const size_t pp = (size_t)(H + 1) * PP;
+    // P' at the block boundaries (+ the corrector scratch Tc when condensed) | GP scratch
+    __host__ __device__ static size_t p_region(int H, int CF) {
+        const int HB = H / CF;
+        const size_t pp = (size_t)(HB + 1) * PP + (CF == 2 ? (size_t)HB * NX : 0);
         return pp > gp_scratch(H) ? pp : gp_scratch(H);
     }
-    __host__ __device__ static size_t lds_doubles(int H) {
+    __host__ __device__ static size_t lds_doubles(int H, int CF) {
+        const int HB = H / CF, NK = CF * NU;   // blocks of the recursions, their inputs
         const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
                               + (size_t)8                    // zero slots (branch-free masked loads)
                               + (size_t)8                    // GP helper command slot
+                              + (lds_mult(CF) ? (size_t)(H + 1) * 2 * NB + (size_t)H * NX : 0)   // multipliers
                               + (size_t)H * NX * GS            // G'_k
-                              + (size_t)H * NU * PS          // K'_k
-                              + (size_t)H * NU * NU          // Ru_k^-1
+                              + (size_t)HB * NK * PS         // K'_j
+                              + (size_t)HB * NK * NK         // Ru_j^-1
                               + (size_t)(H + 1) * NB * 2     // hq, gq
-                              + (size_t)(H + 1) * NX;        // dx (forward sweep)
-        if (kCR) {
-            // no Riccati stores (K', Ru^-1, dx, P', A'): the cyclic-reduction region, aliased by the GP
-            // evaluation scratch (linearisation) and the tightening scratch
-            const size_t base = (size_t)64 + 8 + 8 + (size_t)H * NX * GS + (size_t)(H + 1) * NB * 2;
-            size_t reg = cr_region(H);
-            if (gp_scratch(H) > reg) reg = gp_scratch(H);
-            if (tight_scratch(H) > reg) reg = tight_scratch(H);
-            return base + reg;
-        }
+                              + (size_t)((NW > 1 || CF == 2 ? H : HB) + 1) * NX   // dx (forward sweep: block
+                                                                        // boundaries; condensed: every stage;
+                                                                        // WSPL: the published residual)
+                              + (CF == 2 ? (size_t)H * NX : 0);   // dpi of every stage
         if (kMfma) {
-            // closed-loop A'_k (the tightening scratch and, WSPL, the step-vector exchange Dq alias it)
-            const size_t acl = (size_t)H * NX * PS;
-            return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H))
-                   + (NWAVES > 1 ? 16 : 0);                      // WSPL reduction slots (xs)
+            // CF = 1: closed-loop A'_k; CF = 2: G^_j.  The tightening scratch aliases it, and (WSPL) the
+            // step-vector exchange Dq, which the condensed layout keeps apart (G^ lives through the QP).
+            const size_t acl = CF == 2 ? (size_t)HB * NX * GH : (size_t)HB * NX * PS;
+            return common + p_region(H, CF) + (acl > tight_scratch(H) ? acl : tight_scratch(H))
+                   + (NWAVES > 1 ? 64 + (CF == 2 ? (size_t)(H + 1) * NB : 0) : 0);   // WSPL: xs (+ Dq)
         }
-        return common + p_region(H)                             // P'_k (packed) | GP scratch
-               + (size_t)NX * GS + GS * GS + 2 * NB + NX         // W', M', vectors
+        return common + p_region(H, CF)                         // P'_k (packed) | GP scratch
                + tight_scratch(H)
                + (NWAVES > 1 ? (size_t)(H + 1) * NB + 64 : 0);  // WSPL exchange (Dq, xs)
     }
+    template <int CF>
     __device__ static Lds carve(double* s, int H) {
+        const int HB = H / CF;
+        constexpr int NK = CF * NU;
         Lds L{};
         L.dummy = s; s += 64;
         L.zero = s;  s += 8;
         L.ctrl = reinterpret_cast<int*>(s);  s += 8;
-        L.G = s;   s += (size_t)H * NX * GS;
-        if constexpr (kCR) {
-            L.hq = s;  s += (size_t)(H + 1) * NB;
-            L.gq = s;  s += (size_t)(H + 1) * NB;
-            L.gz = s;
-            L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
-            L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
-            L.gsh = L.gs + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
-            L.cd = s;
-            L.Sig = s + (size_t)H * NUNC;
-            L.Dp = s;  s += (size_t)H * TT;
-            L.Eb = s;  s += cr_eb_blocks(H) * TB;
-            L.XT = s;
-            const size_t xt = (size_t)2 * (H / 2) * TB, tv = (size_t)H * NX;
-            s += xt > tv ? xt : tv;
-            L.RV = s;
-            return L;
+        if constexpr (lds_mult(CF)) {
+            L.lam = s; s += (size_t)(H + 1) * 2 * NB;
+            L.pim = s; s += (size_t)H * NX;
         }
-        L.K = s;   s += (size_t)H * NU * PS;
-        L.Rui = s; s += (size_t)H * NU * NU;
+        L.G = s;   s += (size_t)H * NX * GS;
+        L.K = s;   s += (size_t)HB * NK * PS;
+        L.Rui = s; s += (size_t)HB * NK * NK;
         L.hq = s;  s += (size_t)(H + 1) * NB;
         L.gq = s;  s += (size_t)(H + 1) * NB;
-        L.dxv = s; s += (size_t)(H + 1) * NX;
+        L.dxv = s; s += (size_t)((NW > 1 || CF == 2 ? H : HB) + 1) * NX;
+        if constexpr (CF == 2) {
+            L.dpv = s; s += (size_t)H * NX;
+            L.Tc = s + (size_t)(HB + 1) * PP;   // behind the boundary P' blocks in the P region
+        }
         L.gz = s;
         L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
         L.gsh = L.gs + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         if (kMfma) {
-            L.P = s;   s += p_region(H);
+            L.P = s;   s += p_region(H, CF);
             L.Acl = s;
+            L.Gh = s;
             L.cd = s;
             L.Sig = s + (size_t)H * NUNC;
             if constexpr (NWAVES > 1) {   // Dq: live only inside an IPM iteration's residual phase
                 L.Dq = s;
-                const size_t acl = (size_t)H * NX * PS;
+                const size_t acl = CF == 2 ? (size_t)HB * NX * GH : (size_t)HB * NX * PS;
                 s += acl > tight_scratch(H) ? acl : tight_scratch(H);
+                if constexpr (CF == 2) {
+                    L.Dq = s;
+                    s += (size_t)(H + 1) * NB;
+                }
                 L.xs = s;
             }
         } else {
-            L.P = s;   s += p_region(H);
-            L.W = s;   s += (size_t)NX * GS;
-            L.Ms = s;  s += (size_t)GS * GS;
-            L.vs = s;  s += (size_t)2 * NB + NX;
+            L.P = s;   s += p_region(H, CF);
             L.cd = s;  s += (size_t)H * NUNC;
             L.Sig = s; s += tight_scratch(H) - (size_t)H * NUNC;
             if constexpr (NWAVES > 1) {
@@ -610,271 +582,16 @@ struct SqpKernel {
     // Newton system of the IPM (HPIPM's backward/forward Riccati structure):
     //   min sum_k 1/2 w_k' diag(hq_k) w_k + gq_k' w_k   s.t.  dx_{k+1} = A_k dx_k + B_k du_k + c_k, dx_0 = 0
     // with w_k = [dx_k; du_k], G'_k = [A_k B_k c_k].  Sequential over stages, parallel over the
-    // entries of each stage's small dense products (one lane per entry, uniform code paths).
-    struct Entries {   // per-lane (row, col) of each phase, decoded once per sweep
-        int8_t i1[R1], j1[R1], i2[R2], j2[R2], i3[R3], j3[R3];
-    };
-    __device__ static Entries decode(int lane) {
-        Entries E;
-#pragma unroll
-        for (int r = 0; r < R1; ++r) {
-            const int e = lane + 64 * r;
-            E.i1[r] = e < N1 ? e / GS : -1;
-            E.j1[r] = e < N1 ? e % GS : 0;
-        }
-#pragma unroll
-        for (int r = 0; r < R2; ++r) {  // upper triangle of GS x GS, row-major, minus (NB, NB)
-            int e = lane + 64 * r, i = -1, j = 0;
-            if (e < N2) {
-                i = 0;
-                while (e >= GS - i) { e -= GS - i; ++i; }
-                j = i + e;
-            }
-            E.i2[r] = i;
-            E.j2[r] = j;
-        }
-#pragma unroll
-        for (int r = 0; r < R3; ++r) {  // P' entries (i <= j, j in [0,NX) or j = NB), then K' entries (a, j)
-            int e = lane + 64 * r, i = -1, j = 0;
-            if (e < N3P) {
-                i = 0;
-                while (e >= NX + 1 - i) { e -= NX + 1 - i; ++i; }
-                j = i + e;
-                if (j == NX) j = NB;   // p column
-            } else if (e < N3) {
-                e -= N3P;
-                i = NX + e / PS;       // i >= NX marks a K' entry of input row a = i - NX
-                j = e % PS;
-                if (j == NX) j = NB;
-            }
-            E.i3[r] = i;
-            E.j3[r] = j;
-        }
-        return E;
-    }
-
-    // Phase 1: W'[l][j] = sum_m P'[l][m] G'[m][j] (+ p_l for the c column).
-    __device__ static void phase_W(const Lds& L, const double* Pn, const double* G, const Entries& E) {
-#pragma unroll
-        for (int r = 0; r < R1; ++r) {
-            const int l = E.i1[r], j = E.j1[r];
-            if (l >= 0) {
-                double pr[PS], gc[NX];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) pr[m] = Pn[l <= m ? pidx(l, m) : pidx(m, l)];
-                pr[NX] = Pn[PO + l];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) gc[m] = G[m * GS + j];
-                double acc = (j == NB) ? pr[NX] : 0.0;
-#pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(pr[m], gc[m], acc);
-                L.W[l * GS + j] = acc;
-            }
-        }
-    }
-
-    // Phase 2: M'[i][j] = diag(hq) / gq + sum_l G'[l][i] W'[l][j], upper triangle.
-    __device__ static void phase_M(const Lds& L, const double* G, const double* hq, const double* gq, const Entries& E) {
-#pragma unroll
-        for (int r = 0; r < R2; ++r) {
-            const int i = E.i2[r], j = E.j2[r];
-            if (i >= 0) {
-                double gi[NX], wj[NX];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) { gi[l] = G[l * GS + i]; wj[l] = L.W[l * GS + j]; }
-                double acc = (i == j) ? hq[i] : ((j == NB) ? gq[i] : 0.0);
-#pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(gi[l], wj[l], acc);
-                L.Ms[i * GS + j] = acc;
-            }
-        }
-    }
-
-    __device__ static bool load_Ri(const Lds& L, double (&Ri)[NU][NU]) {
-        double Ru[NU][NU];
-#pragma unroll
-        for (int a = 0; a < NU; ++a)
-#pragma unroll
-            for (int b2 = 0; b2 < NU; ++b2)
-                Ru[a][b2] = L.Ms[(NX + min(a, b2)) * GS + NX + max(a, b2)];
-        return spd_inverse<NU>(Ru, Ri);
-    }
-
-    // M'[NX+b][j] for j in [0,NX) (lower triangle -> read the mirror) or j = NB.
-    __device__ static double mcol(const Lds& L, int b2, int j) {
-        return j < NX ? L.Ms[j * GS + NX + b2] : L.Ms[(NX + b2) * GS + NB];
-    }
-
-    __device__ static bool riccati_factor(const Lds& L, int H, int lane, const Entries& E) {
-        // P'_H = [diag(hq_H[x]) | gq_H[x]]
-        double* PH = L.P + (size_t)H * PP;
-        for (int e = lane; e < NX * PS; e += 64) {
-            const int i = e / PS, j = e % PS;
-            if (j == NX) PH[PO + i] = L.gq[H * NB + i];
-            else if (i <= j) PH[pidx(i, j)] = (i == j) ? L.hq[H * NB + i] : 0.0;
-        }
-        WSYNC();
-        bool ok = true;
-        for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * PP;
-            const double* G = L.G + (size_t)k * NX * GS;
-            phase_W(L, Pn, G, E);
-            WSYNC();
-            phase_M(L, G, L.hq + k * NB, L.gq + k * NB, E);
-            WSYNC();
-            double Ri[NU][NU];
-            ok = load_Ri(L, Ri) && ok;
-            double* Pk = L.P + (size_t)k * PP;
-            double* Kk = L.K + (size_t)k * NU * PS;
-#pragma unroll
-            for (int r = 0; r < R3; ++r) {
-                const int i = E.i3[r], j = E.j3[r];
-                if (i < 0 || (i < NX && k == 0)) continue;   // P_0 is not needed
-                double mj[NU], tr[NU];
-#pragma unroll
-                for (int b2 = 0; b2 < NU; ++b2) mj[b2] = mcol(L, b2, j);
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {   // tr = Ru^-1 M'[u, j]  (no runtime-indexed arrays)
-                    double t = 0.0;
-#pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) t = fma(Ri[a][b2], mj[b2], t);
-                    tr[a] = t;
-                }
-                const int jj = (j == NB) ? NX : j;
-                if (i < NX) {
-                    double mi[NU];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) mi[a] = L.Ms[i * GS + NX + a];
-                    double acc = L.Ms[i * GS + j];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) acc = fma(-mi[a], tr[a], acc);
-                    Pk[jj == NX ? PO + i : pidx(i, j)] = acc;   // entries decode with i <= j
-                } else {
-                    double t = 0.0;
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) t = (i - NX == a) ? tr[a] : t;
-                    Kk[(i - NX) * PS + jj] = -t;
-                }
-            }
-            if (lane < NU * NU) {
-                double rv = 0.0;
-#pragma unroll
-                for (int a = 0; a < NU; ++a)
-#pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) rv = (lane == a * NU + b2) ? Ri[a][b2] : rv;
-                L.Rui[(size_t)k * NU * NU + lane] = rv;
-            }
-            WSYNC();
-        }
-        return ok;
-    }
-
-    // Vector-only backward sweep with the stored factorisation (Mehrotra corrector): p, kff.
-    __device__ static void riccati_vector(const Lds& L, int H, int lane) {
-        if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
-        WSYNC();
-        for (int k = H - 1; k >= 0; --k) {
-            const double* Pn = L.P + (size_t)(k + 1) * PP;
-            const double* G = L.G + (size_t)k * NX * GS;
-            double* pv = L.vs;
-            if (lane < NX) {
-                double pr[PS], c[NX];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) pr[m] = Pn[lane <= m ? pidx(lane, m) : pidx(m, lane)];
-                pr[NX] = Pn[PO + lane];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) c[m] = G[m * GS + NB];
-                double acc = pr[NX];
-#pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(pr[m], c[m], acc);
-                pv[lane] = acc;
-            }
-            WSYNC();
-            // gv_j = gq_kj + sum_l G_lj pv_l ; p_k = gv_x + K' gv_u ; kff = -Ru^-1 gv_u
-            if (lane < NX + NU) {
-                double pvl[NX];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) pvl[l] = pv[l];
-                double gu[NU];
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    double gcol[NX];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) gcol[l] = G[l * GS + NX + a];
-                    double acc = L.gq[k * NB + NX + a];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) acc = fma(gcol[l], pvl[l], acc);
-                    gu[a] = acc;
-                }
-                if (lane < NX) {
-                    if (k >= 1) {
-                        const int i = lane;
-                        double gcol[NX], kc[NU];
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) gcol[l] = G[l * GS + i];
-#pragma unroll
-                        for (int a = 0; a < NU; ++a) kc[a] = L.K[(size_t)k * NU * PS + a * PS + i];
-                        double acc = L.gq[k * NB + i];
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) acc = fma(gcol[l], pvl[l], acc);
-#pragma unroll
-                        for (int a = 0; a < NU; ++a) acc = fma(kc[a], gu[a], acc);
-                        L.P[(size_t)k * PP + PO + i] = acc;
-                    }
-                } else {
-                    const int a = lane - NX;
-                    double ri[NU];
-#pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) ri[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
-                    double t = 0.0;
-#pragma unroll
-                    for (int b2 = 0; b2 < NU; ++b2) t = fma(ri[b2], gu[b2], t);
-                    L.K[(size_t)k * NU * PS + a * PS + NX] = -t;
-                }
-            }
-            WSYNC();
-        }
-    }
-
-    // Forward sweep: dx_0 = 0, du_k = K'_k [dx_k; 1], dx_{k+1} = G'_k [dx_k; du_k; 1].
-    __device__ static void riccati_forward(const Lds& L, int H, int lane) {
-        if (lane < NX) L.dxv[lane] = 0.0;
-        WSYNC();
-        for (int k = 0; k < H; ++k) {
-            if (lane < NX) {
-                const double* G = L.G + (size_t)k * NX * GS;
-                const double* Kk = L.K + (size_t)k * NU * PS;
-                double xk[NX], kr[NU][PS], gr[GS];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) xk[j] = L.dxv[(size_t)k * NX + j];
-#pragma unroll
-                for (int a = 0; a < NU; ++a)
-#pragma unroll
-                    for (int j = 0; j < PS; ++j) kr[a][j] = Kk[a * PS + j];
-#pragma unroll
-                for (int j = 0; j < GS; ++j) gr[j] = G[lane * GS + j];
-                double acc = gr[NB];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) acc = fma(gr[j], xk[j], acc);
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    double du = kr[a][NX];
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) du = fma(kr[a][j], xk[j], du);
-                    acc = fma(gr[NX + a], du, acc);
-                }
-                L.dxv[(size_t)(k + 1) * NX + lane] = acc;
-            }
-            WSYNC();
-        }
-    }
+    // entries of each stage's small dense products: mfma_backward_h (one 16x16 tile per stage) or
+    // mfma_backward_big (two column tiles, quad3d) below; the sweeps with the stored factorisation
+    // on the 4-block MFMA (single tile) or the VALU with readlane broadcasts (wide stages).
 
     // ------------------------------------------------------------------ VALU sweeps in registers (wide stages)
     // Forward sweep dx_0 = 0, du_k = K'_k [dx_k; 1], dx_{k+1} = G'_k [dx_k; du_k; 1] with the state in
     // registers (lane i < NX: dx[i]) and broadcast by v_readlane: every lane forms the x-part of its
     // G' row and lanes NX..NB-1 (a = lane - NX) the input du_a from their K' row, then du is broadcast
     // the same way.  The stage operands (one G' row, one K' row per lane) are loaded a stage ahead.
-    // Replaces riccati_forward's LDS round trip per stage; same output (dxv).
+    // Output: dxv.
     __device__ static void valu_forward_big(const Lds& L, int H, int lane) {
         const int row = lane < NX ? lane : 0;
         const int a = (lane >= NX && lane < NB) ? lane - NX : 0;
@@ -931,7 +648,7 @@ struct SqpKernel {
     //   pv = t_k + p_{k+1} (t_k = P_{k+1} c_k for all stages in parallel first),
     //   lane j < NB: s_j = gq_kj + sum_l G'_k[l][j] pv_l   (x-part of p_k for j < NX, gu_a for j = NX + a),
     //   p_k = s_x + K_k' gu (lanes < NX),  kff_k = -Ru_k^-1 gu (lanes NX..NB-1),
-    // with pv and gu broadcast by v_readlane.  Same outputs as riccati_vector (p in P', kff in K').
+    // with pv and gu broadcast by v_readlane.  Outputs: p in P', kff in K'.
     // Scratch: t aliases hq (rewritten before the next factorisation).
     __device__ static void valu_vector_big(const Lds& L, int H, int lane) {
         double* T = L.hq;
@@ -1011,23 +728,6 @@ struct SqpKernel {
         WSYNC();
     }
 
-    // sweeps of the wide (non-MFMA) path: the register versions above; -DGPMPC_SWEEP_LDS keeps the
-    // LDS-staged riccati_forward / riccati_vector
-    __device__ static void forward_big(const Lds& L, int H, int lane) {
-#ifdef GPMPC_SWEEP_LDS
-        riccati_forward(L, H, lane);
-#else
-        valu_forward_big(L, H, lane);
-#endif
-    }
-    __device__ static void vector_big(const Lds& L, int H, int lane) {
-#ifdef GPMPC_SWEEP_LDS
-        riccati_vector(L, H, lane);
-#else
-        valu_vector_big(L, H, lane);
-#endif
-    }
-
     // Per-lane step of stage k from the Riccati solution: dd = [dx_k; du_k] and dpi_k.
     __device__ static void recover_step(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
         const bool on = lane <= H;
@@ -1075,238 +775,6 @@ struct SqpKernel {
     //   Schur onto the state block       Ru by readlane, row/column slices by lane shuffles
     __device__ static int pidx(int i, int j) { return i * NX - (i * (i - 1)) / 2 + (j - i); }  // i <= j < NX
 
-    // DIAG (tools/ric_micro.hip only): bit 0 drops the P', K', Ru^-1 stores, bit 1 replaces the
-    // Ru inverse chain by a plain move (measures the MFMA chain alone).
-    template <bool kSchurN = false, int DIAG = 0>
-    __device__ static bool mfma_backward(const Lds& L, int H, int lane) {
-        const int lr = lane >> 4, lc = lane & 15;
-        const bool colok = (lc < NX) || (lc == NB);
-        const int jj = (lc == NB) ? NX : lc;
-        // rows NX..NX+NU-1 of the C tile (the u rows of M') sit in element SE of lane groups
-        // SG..SG+NU-1; the Schur operands need them in lane groups 0..NU-1.
-        constexpr int SE = NX >> 2, SG = NX & 3;
-        static_assert(((NX + NU - 1) >> 2) == SE && SG + NU <= 4, "u rows of M' must share one C element");
-        static_assert(NU <= 2, "MFMA Schur path handles NU <= 2");
-        static_assert(NB <= 8 && NX <= 8, "stage operands occupy C elements 0..1");
-        double pn[2];
-        f64x4 pq = {0.0, 0.0, 0.0, 0.0};   // P'_{k+1} as the Schur MFMA left it (rows 8..15 in [2], [3])
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int row = lr + 4 * r;
-            double v = 0.0;
-            if (row < NX) {
-                if (lc < NX) v = (row == lc) ? L.hq[H * NB + row] : 0.0;
-                else if (lc == NB) v = L.gq[H * NB + row];
-            }
-            pn[r] = v;
-        }
-        {   // P'_H (packed) for the multiplier recovery of stage H-1
-            double* PH = L.P + (size_t)H * PP;
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int row = lr + 4 * r;
-                if (row < NX) {
-                    if (lc == NB) PH[NX * (NX + 1) / 2 + row] = pn[r];
-                    else if (lc < NX && row <= lc) PH[pidx(row, lc)] = pn[r];
-                }
-            }
-        }
-        bool ok = true;
-        // Stage operands as per-lane (base, stride) streams: lanes whose entry is structurally zero
-        // read the zero slot with stride 0, so a stage load is one address step and no select.
-        // G'_k row r (< NX), column lc (< GS) -> B operand of W' / A operand of M'.
-        const double* gb[2];
-        int gst[2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const int row = lr + 4 * s2;
-            const bool ok2 = row < NX && lc < GS;
-            gb[s2] = ok2 ? L.G + row * GS + lc : L.zero;
-            gst[s2] = ok2 ? NX * GS : 0;
-        }
-        // C-init of M': hq on the diagonal (rows < NB), gq in column NB
-        const double* db[2];
-        int dst[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int row = lr + 4 * r;
-            const bool dg = row < NB && row == lc, gcol = row < NB && lc == NB;
-            db[r] = dg ? L.hq + row : (gcol ? L.gq + row : L.zero);
-            dst[r] = (dg || gcol) ? NB : 0;
-        }
-        struct Stage { double g[2], d[2]; };
-        // Stages are loaded in the order H-1, H-2, ..., 0: each stream steps back by its per-lane
-        // stride (one subtract per stream and stage instead of a multiply-add on the address).
-        const double* pg[2] = {gb[0] + (H - 1) * gst[0], gb[1] + (H - 1) * gst[1]};
-        const double* pd[2] = {db[0] + (H - 1) * dst[0], db[1] + (H - 1) * dst[1]};
-        auto load_stage = [&](int /* k, consecutive from H-1 down */, Stage& st) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                st.g[q] = *pg[q];
-                pg[q] -= gst[q];
-                st.d[q] = *pd[q];
-                pd[q] -= dst[q];
-            }
-        };
-        // Store streams, stepping back one stage per call (stages are visited H-1 .. 0); entries
-        // that are not stored go to a dummy slot with stride 0.
-        double* sp[2];
-        int sp_st[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int row = lr + 4 * r;
-            const bool st = (row < NX) && colok && ((lc == NB) || row <= lc);
-            const int idx = (lc == NB) ? NX * (NX + 1) / 2 + row : pidx(row < lc ? row : lc, row < lc ? lc : row);
-            sp[r] = st ? L.P + (H - 1) * PP + idx : L.dummy + lane;
-            sp_st[r] = st ? PP : 0;
-        }
-        const bool kst = lr < NU && colok;
-        double* sk = kst ? L.K + (H - 1) * NU * PS + lr * PS + jj : L.dummy + lane;
-        const int sk_st = kst ? NU * PS : 0;
-        const bool rst = lane < NU * NU;
-        double* srui = rst ? L.Rui + (H - 1) * NU * NU + lane : L.dummy + lane;
-        const int srui_st = rst ? NU * NU : 0;
-        // DIAG bit 2: the stores of stage k are issued inside stage k-1, after its W' products
-        // (off the recursion's dependency chain), and the K' chain is rcp -> e -> fma -> fma
-        constexpr bool kDefer = (DIAG & 4) != 0;
-        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
-        bool pend = false;
-        auto flush = [&]() {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                *sp[r] = pend_p[r];
-                sp[r] -= sp_st[r];
-            }
-            *sk = pend_k;
-            sk -= sk_st;
-            *srui = pend_r;
-            srui -= srui_st;
-        };
-        auto stage = [&](int k, const Stage& sd) {
-            // W' = P'_{k+1} G'_k (p_{k+1} enters as the C-init of column NB), M' = G'^T W' + [diag(hq) | gq]
-            // rows 8..15 of W' are never read (M' takes w[0], w[1]), so their C-init is P'_{k+1}'s own
-            // (finite) rows 8..15: the C quad is two selects on the P' quad, no zero fill
-            const f64x4 cw = {lc == NB ? pn[0] : 0.0, lc == NB ? pn[1] : 0.0, pq[2], pq[3]};
-            // (A operand = P' itself: its p column, lane column NB, only feeds row NB of W', which
-            // the M' product never reads, so it needs no mask)
-            f64x4 w = mfma64(pn[0], sd.g[0], cw);
-            w = mfma64(pn[1], sd.g[1], w);
-            if constexpr (kDefer) {
-                if (pend) flush();
-                pend = true;
-            }
-            f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], 0.0, 0.0});
-            m = mfma64(sd.g[1], w[1], m);
-            // Ru = M'_uu by readlane.  K' = -Ru^-1 M'_u through the adjugate: the numerators are
-            // formed beside det and its reciprocal, so after det the dependency chain of the
-            // recursion is rcp -> cubic refinement -> one multiply.
-            double Ru[NU][NU];
-#pragma unroll
-            for (int a = 0; a < NU; ++a)
-#pragma unroll
-                for (int b2 = a; b2 < NU; ++b2) {
-                    if constexpr ((DIAG & 2) != 0) Ru[a][b2] = (a == b2) ? 1.0 : 0.0;
-                    else Ru[a][b2] = readlane_d(m[SE], ((SG + a) << 4) | (NX + b2));
-                    Ru[b2][a] = Ru[a][b2];
-                }
-            // mu: lane (a, c) <- M'[NX + a][c]; A operand of the Schur product (M'_xu by symmetry).
-            // Only lanes a < NU need it (the A operand is masked), so the upper-half move needs no select.
-            double mu;
-            if constexpr (SG == 0) mu = m[SE];
-            else if constexpr (SG == 2) mu = from_upper_half(m[SE]);
-            else mu = __shfl(m[SE], (((lr + SG) & 3) << 4) | lc);
-            // B operand: K'[a][c] = -sum_b Ri[a][b] M'[NX + b][c]  (feedback K and feedforward kff);
-            // rows a >= NU meet a zero A operand and need no mask
-            double kb, Ri[NU][NU], num = 0.0, id = 0.0;
-            if constexpr (NU == 1) {
-                ok = ok && (Ru[0][0] > 0.0);
-                id = fast_rcp(Ru[0][0]);
-                Ri[0][0] = id;
-                num = mu;
-                kb = -id * mu;
-            } else {
-                const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
-                ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
-                // lane a=0: mu = M'[NX], mo = M'[NX+1]; lane a=1: mu = M'[NX+1], mo = M'[NX]
-                const double mo = xor16_d(mu);
-                num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);   // adj(Ru) M'_u
-                if constexpr (kDefer) {
-                    // id = r (1 + e + e^2): kb = t + t (e + e^2) with t = -num r beside e
-                    const double r0 = __builtin_amdgcn_rcp(det);
-                    const double e = fma(-det, r0, 1.0);
-                    const double ee = fma(e, e, e);
-                    const double t = num * -r0;
-                    id = fma(r0, ee, r0);
-                    kb = fma(t, ee, t);
-                } else {
-                    id = fast_rcp(det);
-                    kb = num * -id;
-                }
-                Ri[0][0] = Ru[1][1] * id;
-                Ri[1][1] = Ru[0][0] * id;
-                Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
-            }
-            if constexpr ((DIAG & 1) == 0) {   // Ru^-1 of stage k (lanes 0..NU*NU-1; Ri is symmetric)
-                double rv = Ri[0][0];
-                if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
-                if constexpr (kDefer) {
-                    pend_r = rv;
-                } else {
-                    *srui = rv;
-                    srui -= srui_st;
-                }
-            }
-            if constexpr ((DIAG & 2) != 0) kb = -mu * 1e-3;
-            // P'_k = M'_x[x|c] + M'_xu K'   (one MFMA, C-init = M').  kSchurN: the numerator product
-            // N = M'_xu adj(Ru) M'_u runs on the matrix core while det / rcp run on the VALU, and
-            // P'_k = M' - N / det is one fma per register (rows 8..15 keep M', finite and unread).
-            f64x4 pk;
-            if constexpr (kSchurN) {
-                const f64x4 nk = mfma64(lr < NU ? mu : 0.0, num, f64x4{0.0, 0.0, 0.0, 0.0});
-                pk = f64x4{fma(-id, nk[0], m[0]), fma(-id, nk[1], m[1]), m[2], m[3]};
-            } else {
-                pk = mfma64(lr < NU ? mu : 0.0, kb, m);
-            }
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                // branch-free store: entries that are not stored go to a dummy slot
-                if constexpr (kDefer) {
-                    pend_p[r] = pk[r];
-                } else if constexpr ((DIAG & 1) == 0) {
-                    *sp[r] = pk[r];
-                    sp[r] -= sp_st[r];
-                }
-                // P'_k is the next stage's A operand unmasked: its entries outside rows < NX and
-                // columns {< NX, NB} are finite and only reach W' rows the M' product never reads
-                // (u columns / rows >= NB) or meet the zero rows >= NX of the G' operand, so the
-                // result is the same as with them zeroed and the select stays off the chain.
-                pn[r] = pk[r];
-            }
-            pq = pk;
-            if constexpr (kDefer) {
-                pend_k = kb;
-            } else if constexpr ((DIAG & 1) == 0) {
-                *sk = kb;
-                sk -= sk_st;
-            }
-        };
-        // stage k's operands are loaded one stage ahead (explicit double buffer: no register
-        // copies that would force the wait right after the load)
-        Stage s0, s1;
-        load_stage(H - 1, s0);
-        int k = H - 1;
-        for (; k >= 1; k -= 2) {
-            load_stage(k - 1, s1);
-            stage(k, s0);
-            if (k >= 2) load_stage(k - 2, s0);
-            stage(k - 1, s1);
-        }
-        if (k == 0) stage(0, s0);
-        if constexpr (kDefer) flush();
-        if constexpr ((DIAG & 3) != 0) L.dummy[lane] = pn[0] + pn[1];   // keeps the chain alive without the stores
-        return ok;
-    }
-
     // Riccati factorisation on v_mfma_f64_16x16x4 in the homogeneous tile layout: tile index t of
     // the 16-wide operands is x_t for t < NX, the affine "1" at CI = NX, u_a at UI + a (UI = 8),
     // zero elsewhere.  The affine column c of G'_k becomes row/column CI of [G'_k; e_CI]
@@ -1317,8 +785,7 @@ struct SqpKernel {
     // stand: no select or copy between the Schur product and the next W' on the recursion.
     // The u rows sit at 8..8+NU-1 = lane groups 0..NU-1 of element 2: the Schur A operand needs no
     // lane move.  Stores of stage k are issued after stage k-1's W' products (sched_barrier), off
-    // the chain.  Outputs identical in format to mfma_backward (packed P', K', Ru^-1).
-    template <int DIAG = 0>
+    // the chain.  Outputs: packed P', K' = [K | kff], Ru^-1 per stage.
     __device__ static bool mfma_backward_h(const Lds& L, int H, int lane) {
         const int lr = lane >> 4, lc = lane & 15;
         constexpr int CI = NX, UI = 8;
@@ -1406,38 +873,29 @@ struct SqpKernel {
         const int srui_st = rst ? NU * NU : 0;
         double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
         bool pend = false;
-        // DIAG (tools/ric_micro.hip): bit 3 drops only the P' stores, bit 4 flushes without the
-        // scheduling barriers, bit 5 flushes after the M' products instead of the W' products
         auto flush = [&]() {
-            if constexpr ((DIAG & 8) == 0) {
 #pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    *sp[r] = pend_p[r];
-                    sp[r] -= sp_st[r];
-                }
+            for (int r = 0; r < 2; ++r) {
+                *sp[r] = pend_p[r];
+                sp[r] -= sp_st[r];
             }
             *sk = pend_k;
             sk -= sk_st;
             *srui = pend_r;
             srui -= srui_st;
         };
-        auto flush_at = [&]() {
-            if constexpr ((DIAG & 16) != 0) {
-                if (pend) flush();
-            } else {
-                __builtin_amdgcn_sched_barrier(0);
-                if (pend) flush();
-                __builtin_amdgcn_sched_barrier(0);
-            }
+        auto flush_at = [&]() {   // the previous stage's stores, pinned after the W' products
+            __builtin_amdgcn_sched_barrier(0);
+            if (pend) flush();
+            __builtin_amdgcn_sched_barrier(0);
             pend = true;
         };
         auto stage = [&](const Stage& sd) {
             f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
             w = mfma64(pn[1], sd.g[1], w);
-            if constexpr ((DIAG & 1) == 0 && (DIAG & 32) == 0) flush_at();
+            flush_at();
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
             m = mfma64(sd.g[1], w[1], m);
-            if constexpr ((DIAG & 1) == 0 && (DIAG & 32) != 0) flush_at();
             double Ru[NU][NU];
 #pragma unroll
             for (int a = 0; a < NU; ++a)
@@ -1489,9 +947,551 @@ struct SqpKernel {
             stage(s1);
         }
         if (k == 0) stage(s0);
-        if constexpr ((DIAG & 1) == 0) flush();
-        else L.dummy[lane] = pn[0] + pn[1];
+        flush();
         return ok;
+    }
+
+    // ------------------------------------------------------------------ condensed Riccati (kCond, H even)
+    // Block j = stages k0 = 2j, k1 = 2j + 1 with the block input z = [x_k0; u_k0; u_k1; 1] in the tile
+    // layout x_t (t < NX), CI = NX, u_k0 at UI .. UI+NU-1, u_k1 at UI+NU .. UI+NCU-1 (UI = 8).  With
+    // T = [G'_k0; e_CI] (x_k1 = T z) and the condensed dynamics x_2j+2 = G^_j z,
+    //   G^_j = A_k1 T + B_k1 (u_k1 slots) + c_k1 e_CI^T        (stored per block: [G^_x | c^ | G^_u]),
+    // the block's cost-to-go is  M = G^''^T P'_{j+1} G^'' + E^T E + D^  with
+    //   E (tile rows 8 + m, m < NX):  sqrt(h_m) T[m][.] + (g_m / sqrt(h_m)) e_CI^T   (h, g: hq, gq of x_k1),
+    // so E^T E = T^T diag(h) T plus the gradient terms in row/column CI (the (CI, CI) entry is a
+    // constant of the cost-to-go, never read), and D^ the diagonal / gradient of x_k0, u_k0, u_k1.
+    // On v_mfma_f64_16x16x4: W = P' G^'' (2 MFMAs), M = G^''^T W over K-steps 0..1 on top of
+    // E^T E + D^ (K-steps 2..3, whose W rows are E itself: the identity block of the stacked system),
+    // then Ru = M_uu (NCU x NCU), K^' = -Ru^-1 M_u and P'_j = M + M_.u K^' (1 MFMA) as in
+    // mfma_backward_h: five dependent MFMA links per block instead of ten per stage pair.  The next
+    // block's operands are 11 LDS loads issued behind the W products; its E^T E products run on the
+    // matrix core while the VALU forms Ru^-1.  Outputs: packed P' at the block boundaries,
+    // K^'_j = [K^ | kff^] (NCU rows), Ru_j^-1 (NCU x NCU).
+    // Everything else of the Newton solve works on G^ without forming the closed-loop maps:
+    // A^_j = [G^_x + G^_u K^_j | c^ + G^_u kff^_j] enters the 4-block MFMA sweeps entry by entry.
+
+    // G^_j rows (one (j, r) per lane and pass).  withx: all columns (once per SQP iteration: G^_x and
+    // G^_u depend on the linearisation only); otherwise the affine column c^ (every IPM iteration:
+    // c_k is the current dynamics residual, column NB of G').
+    template <bool withx>
+    __device__ static void cond_ghat(const Lds& L, int H, int lane) {
+        const int HB = H >> 1;
+        for (int e = lane; e < HB * NX; e += 64) {
+            const int j = e / NX, r = e - j * NX;
+            const double* G0 = L.G + (size_t)(2 * j) * NX * GS;
+            const double* g1 = G0 + NX * GS + r * GS;
+            double a1[NX];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) a1[m] = g1[m];
+            auto col = [&](int c) {
+                double acc = 0.0;
+#pragma unroll
+                for (int m = 0; m < NX; ++m) acc = fma(a1[m], G0[m * GS + c], acc);
+                return acc;
+            };
+            double* out = L.Gh + (size_t)e * GH;
+            if constexpr (withx) {
+                double o[GH];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) o[c] = col(c);
+                o[NX] = col(NB) + g1[NB];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    o[NX + 1 + a] = col(NX + a);
+                    o[NX + 1 + NU + a] = g1[NX + a];
+                }
+#pragma unroll
+                for (int c = 0; c < GH; ++c) out[c] = o[c];
+            } else {
+                out[NX] = col(NB) + g1[NB];
+            }
+        }
+    }
+
+    __device__ static bool cond_backward(const Lds& L, int H, int lane) {
+        if constexpr (!kCond) {
+            return false;
+        } else {
+        const int lr = lane >> 4, lc = lane & 15;
+        constexpr int CI = NX, UI = 8;
+        static_assert(NX + 1 <= 8 && UI + NCU <= 12 && UI + NX <= 16, "condensed tile layout");
+        const int HB = H >> 1;
+        // tile column lc: the G' column of T = G''_k0 it reads and the G^ column (-1: none)
+        const int gc0 = lc < NX ? lc : (lc == CI ? NB : ((lc >= UI && lc < UI + NU) ? NX + lc - UI : -1));
+        const int hc = lc < NX ? lc : (lc == CI ? NX : ((lc >= UI && lc < UI + NCU) ? NX + 1 + lc - UI : -1));
+        // block variable of tile slot t: (stage offset i, stage variable v), or v = -1
+        auto bvar = [](int t, int& i) {
+            i = 0;
+            if (t < NX) return t;
+            if (t >= UI && t < UI + NCU) { i = (t - UI) / NU; return NX + (t - UI) % NU; }
+            return -1;
+        };
+        double pn[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {   // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
+            const int t = lr + 4 * r;
+            double v = 0.0;
+            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
+            else if (t < NX && lc == CI) v = L.gq[H * NB + t];
+            else if (t == CI && lc < NX) v = L.gq[H * NB + lc];
+            pn[r] = v;
+        }
+        {   // P'_H (packed, boundary HB) for the multipliers of stage H-1
+            double* PH = L.P + (size_t)HB * PP;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int t = lr + 4 * r;
+                if (t < NX) {
+                    if (lc == CI) PH[PO + t] = pn[r];
+                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
+                }
+            }
+        }
+        bool ok = true;
+        // operand streams, blocks HB-1 .. 0 (masked entries read the zero / one slots with stride 0)
+        const double* pg[2];    // G^'' rows lr + 4q, column lc
+        const double* pt[2];    // T rows m = lr + 4q, column lc
+        const double* ph[2];    // hq, gq of x_k1[m]
+        const double* pq[2];
+        int gst[2], tst[2], hst[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int r = lr + 4 * q;
+            const bool ld = r < NX && hc >= 0, one = r == CI && lc == CI;
+            pg[q] = ld ? L.Gh + ((size_t)(HB - 1) * NX + r) * GH + hc : L.zero + (one ? 7 : 0);
+            gst[q] = ld ? NX * GH : 0;
+            const bool lt = r < NX && gc0 >= 0;
+            pt[q] = lt ? L.G + (size_t)(2 * HB - 2) * NX * GS + r * GS + gc0 : L.zero;
+            tst[q] = lt ? 2 * NX * GS : 0;
+            const bool lh = r < NX;
+            ph[q] = lh ? L.hq + (size_t)(2 * HB - 1) * NB + r : L.zero + 7;   // masked: h = 1, g = 0
+            pq[q] = lh ? L.gq + (size_t)(2 * HB - 1) * NB + r : L.zero;
+            hst[q] = lh ? 2 * NB : 0;
+        }
+        const double* pd[3];   // D^ (rows lr + 4r, r = 0..2)
+        int dst[3];
+        int ilc;
+        const int vlc = bvar(lc, ilc);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int t = lr + 4 * r;
+            int it;
+            const int vt = bvar(t, it);
+            const double* base = L.zero;
+            bool on = false;
+            if (vt >= 0 && t == lc) { base = L.hq + it * NB + vt; on = true; }
+            else if (vt >= 0 && lc == CI) { base = L.gq + it * NB + vt; on = true; }
+            else if (t == CI && vlc >= 0) { base = L.gq + ilc * NB + vlc; on = true; }
+            pd[r] = on ? base + (size_t)(2 * HB - 2) * NB : L.zero;
+            dst[r] = on ? 2 * NB : 0;
+        }
+        struct Raw { double g[2], t[2], h[2], q[2], d[3]; };
+        struct Blk { double g[2]; f64x4 mb; };
+        auto load = [&](Raw& rw) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                rw.g[q] = *pg[q];
+                pg[q] -= gst[q];
+                rw.t[q] = *pt[q];
+                pt[q] -= tst[q];
+                rw.h[q] = *ph[q];
+                ph[q] -= hst[q];
+                rw.q[q] = *pq[q];
+                pq[q] -= hst[q];
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                rw.d[r] = *pd[r];
+                pd[r] -= dst[r];
+            }
+        };
+        // E rows and E^T E + D^ (K-steps 2, 3 of M: independent of P')
+        auto make = [&](const Raw& rw, Blk& bk) {
+            double e[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const double sh = __builtin_sqrt(rw.h[q]);
+                e[q] = fma(sh, rw.t[q], lc == CI ? rw.q[q] * fast_rcp(sh) : 0.0);
+                bk.g[q] = rw.g[q];
+            }
+            bk.mb = mfma64(e[0], e[0], f64x4{rw.d[0], rw.d[1], rw.d[2], 0.0});
+            bk.mb = mfma64(e[1], e[1], bk.mb);
+        };
+        // store streams (blocks HB-1 .. 0), dummy slot with stride 0 for entries not stored
+        double* sp[2];
+        int sp_st[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int t = lr + 4 * r;
+            const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc));
+            const int idx = (lc == CI) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
+            sp[r] = st ? L.P + (size_t)(HB - 1) * PP + idx : L.dummy + lane;
+            sp_st[r] = st ? PP : 0;
+        }
+        const bool kst = lr < NCU && (lc < NX || lc == CI);
+        double* sk = kst ? L.K + (size_t)(HB - 1) * NCU * PS + lr * PS + (lc == CI ? NX : lc) : L.dummy + lane;
+        const int sk_st = kst ? NCU * PS : 0;
+        const bool rst = lr < NCU && lc < NCU;
+        double* srui = rst ? L.Rui + (size_t)(HB - 1) * NCU * NCU + lr * NCU + lc : L.dummy + lane;
+        const int srui_st = rst ? NCU * NCU : 0;
+        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
+        bool pend = false;
+        auto flush = [&]() {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                *sp[r] = pend_p[r];
+                sp[r] -= sp_st[r];
+            }
+            *sk = pend_k;
+            sk -= sk_st;
+            *srui = pend_r;
+            srui -= srui_st;
+        };
+        // one block: the chain W -> M -> Ru^-1 -> Schur; the next block's loads behind W, its E^T E
+        // while the VALU forms Ru^-1
+        Raw rw;
+        auto block = [&](const Blk& cb, Blk& nb, bool more) {
+            f64x4 w = mfma64(pn[0], cb.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
+            w = mfma64(pn[1], cb.g[1], w);
+            __builtin_amdgcn_sched_barrier(0);
+            if (pend) flush();
+            pend = true;
+            if (more) load(rw);
+            __builtin_amdgcn_sched_barrier(0);
+            f64x4 m = mfma64(cb.g[0], w[0], cb.mb);
+            m = mfma64(cb.g[1], w[1], m);
+            __builtin_amdgcn_sched_barrier(0);
+            if (more) make(rw, nb);
+            __builtin_amdgcn_sched_barrier(0);
+            const double mu = m[2];          // lane (q, c) <- M[UI + q][c]
+            double kb, rv;
+            if constexpr (NCU == 2) {
+                const double r00 = readlane_d(mu, UI), r01 = readlane_d(mu, UI + 1), r11 = readlane_d(mu, 16 + UI + 1);
+                const double det = r00 * r11 - r01 * r01;
+                ok = ok && (r00 > 0.0) && (det > 0.0);
+                const double mo = xor16_d(mu);
+                const double num = fma((lr & 1) ? r00 : r11, mu, -r01 * mo);   // adj(Ru) M_u
+                const double r0 = __builtin_amdgcn_rcp(det);
+                const double e = fma(-det, r0, 1.0);
+                const double ee = fma(e, e, e);
+                const double t = num * -r0;
+                const double id = fma(r0, ee, r0);
+                kb = fma(t, ee, t);
+                rv = (lane == 0) ? r11 * id : ((lane == 17) ? r00 * id : -r01 * id);
+            } else {
+                // Ru^-1 by 2x2 blocks [[A, B], [B^T, C]] (as mfma_backward_big)
+                const double a00 = readlane_d(mu, UI), a01 = readlane_d(mu, UI + 1), a11 = readlane_d(mu, 16 + UI + 1);
+                const double b00 = readlane_d(mu, UI + 2), b01 = readlane_d(mu, UI + 3), b10 = readlane_d(mu, 16 + UI + 2),
+                             b11 = readlane_d(mu, 16 + UI + 3);
+                const double c00 = readlane_d(mu, 32 + UI + 2), c01 = readlane_d(mu, 32 + UI + 3),
+                             c11 = readlane_d(mu, 48 + UI + 3);
+                const double dA = fma(a00, a11, -a01 * a01);
+                const double iA = fast_rcp(dA);
+                const double A00 = a11 * iA, A01 = -a01 * iA, A11 = a00 * iA;
+                const double X00 = fma(A00, b00, A01 * b10), X01 = fma(A00, b01, A01 * b11);
+                const double X10 = fma(A01, b00, A11 * b10), X11 = fma(A01, b01, A11 * b11);
+                const double S00 = c00 - fma(b00, X00, b10 * X10), S01 = c01 - fma(b00, X01, b10 * X11);
+                const double S11 = c11 - fma(b01, X01, b11 * X11);
+                const double dS = fma(S00, S11, -S01 * S01);
+                ok = ok && (a00 > 0.0) && (dA > 0.0) && (dS > 0.0);
+                const double iS = fast_rcp(dS);
+                const double C00 = S11 * iS, C01 = -S01 * iS, C11 = S00 * iS;
+                const double Y00 = fma(X00, C00, X01 * C01), Y01 = fma(X00, C01, X01 * C11);
+                const double Y10 = fma(X10, C00, X11 * C01), Y11 = fma(X10, C01, X11 * C11);
+                const double Z00 = A00 + fma(Y00, X00, Y01 * X01), Z01 = A01 + fma(Y00, X10, Y01 * X11);
+                const double Z11 = A11 + fma(Y10, X10, Y11 * X11);
+                const int a = lr;   // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a, column a ^ t
+                const double c0 = (a == 0) ? Z00 : ((a == 1) ? Z11 : ((a == 2) ? C00 : C11));
+                const double c1 = (a & 2) ? C01 : Z01;
+                const double c2 = (a & 1) ? -Y11 : -Y00;
+                const double c3 = ((a ^ (a >> 1)) & 1) ? -Y10 : -Y01;
+                const double v1 = xor16_d(mu), v2 = xor32_d(mu), v3 = xor32_d(v1);   // rows UI + (a ^ 1, 2, 3)
+                kb = -fma(c0, mu, fma(c1, v1, fma(c2, v2, c3 * v3)));
+                const int tt = lc ^ a;
+                rv = (tt == 0) ? c0 : ((tt == 1) ? c1 : ((tt == 2) ? c2 : c3));
+            }
+            const f64x4 pk = mfma64(lr < NCU ? mu : 0.0, kb, m);   // P'_j = M + M_.u K^'
+            pend_p[0] = pk[0];
+            pend_p[1] = pk[1];
+            pend_k = kb;
+            pend_r = rv;
+            pn[0] = pk[0];
+            pn[1] = pk[1];
+        };
+        Blk b0, b1;
+        load(rw);
+        make(rw, b0);
+        int j = HB - 1;
+        for (; j >= 1; j -= 2) {   // two blocks per iteration (ping-pong: no register copies)
+            block(b0, b1, true);
+            block(b1, b0, j >= 2);
+        }
+        if (j == 0) block(b0, b1, false);
+        flush();
+        return ok;
+        }
+    }
+
+    // One entry of the closed-loop block map A^_j = [G^_x + G^_u K^_j | c^ + G^_u kff^_j] for the
+    // 4-block sweeps: row r, column c (c = NX: the affine column), from G^_j and K^_j.
+    struct CondOp { double g, b[NCU], k[NCU]; };
+    __device__ static void cond_op_load(const double* gr, const double* kc, int c, CondOp& op) {
+        op.g = gr[c];
+#pragma unroll
+        for (int q = 0; q < NCU; ++q) {
+            op.b[q] = gr[NX + 1 + q];
+            op.k[q] = kc[q * PS];
+        }
+    }
+    __device__ static double cond_op(const CondOp& op) {
+        double acc = op.g;
+#pragma unroll
+        for (int q = 0; q < NCU; ++q) acc = fma(op.b[q], op.k[q], acc);
+        return acc;
+    }
+
+    // Forward sweep over the blocks: dx_2j+2 = A^_j [dx_2j; 1] on the 4-block MFMA (mfma4_stage), the
+    // stage operand A^_j[row][col] formed from G^_j and K^_j a block ahead; dx at the boundaries.
+    __device__ static void cond_forward(const Lds& L, int H, int lane) {
+        const int HB = H >> 1;
+        const Mfma4Lane q = mfma4_lane(lane);
+        const bool ld = q.row < NX && q.col <= NX;
+        const bool one = q.row == NX && q.col == NX;
+        const double* gr = L.Gh + (size_t)(ld ? q.row : 0) * GH;   // row of G^_j (stride NX GH per block)
+        const double* kc = L.K + (ld ? q.col : 0);                  // column of K^_j (stride NCU PS)
+        const int gcol = q.col < NX ? q.col : NX;
+        const int gs = ld ? NX * GH : 0, ks = ld ? NCU * PS : 0;
+        const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+        const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+        double* out = stlo ? L.dxv + 2 * NX + q.r : (sthi ? L.dxv + 2 * NX + 4 + q.r : L.dummy + lane);
+        const int ost = (stlo || sthi) ? 2 * NX : 0;
+        if (lane < NX) L.dxv[lane] = 0.0;
+        double y = mfma4_vec(q, [](int) { return 0.0; });
+        CondOp o0, o1;
+        cond_op_load(gr, kc, gcol, o0);
+        auto step = [&](const CondOp& op) {
+            const double a = ld ? cond_op(op) : (one ? 1.0 : 0.0);
+            double sv;
+            y = mfma4_stage(a, y, sv);
+            *out = sv;
+            out += ost;
+        };
+        int j = 0;
+        for (; j + 1 < HB; j += 2) {
+            gr += gs;
+            kc += ks;
+            cond_op_load(gr, kc, gcol, o1);
+            step(o0);
+            if (j + 2 < HB) {
+                gr += gs;
+                kc += ks;
+                cond_op_load(gr, kc, gcol, o0);
+            }
+            step(o1);
+        }
+        if (j < HB) step(o0);
+    }
+
+    // Interior states and every stage's dynamics multipliers from the boundary states (all entries
+    // in parallel): dx_2j+1 = A_k0 dx_2j + B_k0 du_k0 + c_k0 (du_k0 = K^_j rows 0..NU-1 [dx_2j; 1]),
+    // dpi_2j+1 = -(P_{j+1} dx_2j+2 + p_{j+1}), then
+    // dpi_2j = A_k1^T dpi_2j+1 - hq_k1,x dx_2j+1 - gq_k1,x (stationarity at x_k1).
+    __device__ static void cond_expand(const Lds& L, int H, int lane) {
+        const int HB = H >> 1, n = HB * NX;
+        for (int e = lane; e < 2 * n; e += 64) {
+            const int f = e < n ? e : e - n, j = f / NX, i = f - j * NX;
+            if (e < n) {
+                const double* x0 = L.dxv + (size_t)(2 * j) * NX;
+                const double* Kj = L.K + (size_t)j * NCU * PS;
+                const double* g0 = L.G + (size_t)(2 * j) * NX * GS + i * GS;
+                double xv[NX];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) xv[c] = x0[c];
+                double acc = g0[NB];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) acc = fma(g0[c], xv[c], acc);
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double du = Kj[a * PS + NX];
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) du = fma(Kj[a * PS + c], xv[c], du);
+                    acc = fma(g0[NX + a], du, acc);
+                }
+                L.dxv[(size_t)(2 * j + 1) * NX + i] = acc;
+            } else {
+                const double* Pn = L.P + (size_t)(j + 1) * PP;
+                const double* xn = L.dxv + (size_t)(2 * j + 2) * NX;
+                double acc = Pn[PO + i];
+#pragma unroll
+                for (int c = 0; c < NX; ++c) acc = fma(Pn[i <= c ? pidx(i, c) : pidx(c, i)], xn[c], acc);
+                L.dpv[(size_t)(2 * j + 1) * NX + i] = -acc;
+            }
+        }
+        WSYNC();
+        for (int e = lane; e < n; e += 64) {
+            const int j = e / NX, i = e - j * NX, k1 = 2 * j + 1;
+            const double* g1 = L.G + (size_t)k1 * NX * GS;
+            const double* p1 = L.dpv + (size_t)k1 * NX;
+            double acc = -fma(L.hq[k1 * NB + i], L.dxv[(size_t)k1 * NX + i], L.gq[k1 * NB + i]);
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(g1[l * GS + i], p1[l], acc);
+            L.dpv[(size_t)(2 * j) * NX + i] = acc;
+        }
+        WSYNC();
+    }
+
+    // Step of stage kq from the condensed solution: dx (every stage expanded), du from K^ of its
+    // block, dpi (every stage expanded).
+    __device__ static void recover_cond(const Lds& L, int H, int kq, double (&dd)[NB], double (&dpi)[NX]) {
+        const int k = min(kq, H), j = min(k >> 1, (H >> 1) - 1), sl = (k & 1) * NU;
+        double x0[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            dd[i] = L.dxv[(size_t)k * NX + i];
+            x0[i] = L.dxv[(size_t)(2 * j) * NX + i];
+            dpi[i] = kq < H ? L.dpv[(size_t)k * NX + i] : 0.0;
+        }
+        const double* Kj = L.K + (size_t)j * NCU * PS + sl * PS;
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double du = Kj[a * PS + NX];
+#pragma unroll
+            for (int c = 0; c < NX; ++c) du = fma(Kj[a * PS + c], x0[c], du);
+            dd[NX + a] = kq < H ? du : 0.0;
+        }
+    }
+
+    // Corrector with the condensed factorisation unchanged (mfma4_vector_backward over blocks):
+    //   p_j = vt_j + A^_j,x^T p_{j+1},  vt_j = q^_j + K^_j^T r^_j + A^_j,x^T t_j,  t_j = P_{j+1} c^_j,
+    //   kff^_j = -Ru_j^-1 (r^_j + G^_u^T (t_j + p_{j+1})),
+    // with [q^; r^] the block gradient (column CI of T^T D_x,k1 T + D^ at the current gq):
+    //   grad^[t] = sum_m T[m][t] (h_m c_k0[m] + g_m) + D^[t][CI].
+    // Scratch: q^ | r^ in dpv (rewritten by cond_expand after the sweep), t in Tc, vt in dxv.
+    __device__ static void cond_vector_backward(const Lds& L, int H, int lane) {
+        const int HB = H >> 1;
+        double* QH = L.dpv;                     // [HB][NX]
+        double* RH = L.dpv + (size_t)HB * NX;   // [HB][NCU]
+        constexpr int NT = NX + NCU;
+        // C1: block gradients (one (j, t) per lane) and t_j = P_{j+1} c^_j (one (j, i) per lane)
+        for (int e = lane; e < HB * (NT + NX); e += 64) {
+            if (e < HB * NT) {
+                const int j = e / NT, t = e - j * NT;   // t < NX: x_k0[t]; else input slot q = t - NX
+                const int k0 = 2 * j, k1 = k0 + 1;
+                const double* G0 = L.G + (size_t)k0 * NX * GS;
+                const int q = t - NX;
+                const bool tin = t < NX || q < NU;      // x_k0 or u_k0: a column of T
+                const int gcol = t < NX ? t : NX + (q < NU ? q : 0);
+                double acc = 0.0;
+#pragma unroll
+                for (int m = 0; m < NX; ++m) {
+                    const double w = fma(L.hq[k1 * NB + m], G0[m * GS + NB], L.gq[k1 * NB + m]);
+                    acc = fma(G0[m * GS + gcol], w, acc);
+                }
+                acc = tin ? acc : 0.0;
+                const int st = (t >= NX && q >= NU) ? k1 : k0;
+                const int v = t < NX ? t : NX + (q < NU ? q : q - NU);
+                acc += L.gq[st * NB + v];
+                if (t < NX) QH[(size_t)j * NX + t] = acc;
+                else RH[(size_t)j * NCU + q] = acc;
+            } else {
+                const int f = e - HB * NT, j = f / NX, i = f - j * NX;
+                const double* Pn = L.P + (size_t)(j + 1) * PP;
+                const double* gh = L.Gh + (size_t)j * NX * GH;
+                double acc = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], gh[l * GH + NX], acc);
+                L.Tc[f] = acc;
+            }
+        }
+        WSYNC();
+        // C2: vt_j[i] = q^[i] + sum_q K^[q][i] (r^[q] + (G^_u^T t)[q]) + (G^_x^T t)[i]   (into dxv)
+        for (int e = lane; e < HB * NX; e += 64) {
+            const int j = e / NX, i = e - j * NX;
+            const double* gh = L.Gh + (size_t)j * NX * GH;
+            const double* Kj = L.K + (size_t)j * NCU * PS;
+            const double* tj = L.Tc + (size_t)j * NX;
+            double tv[NX];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) tv[l] = tj[l];
+            double acc = QH[e];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(gh[l * GH + i], tv[l], acc);
+#pragma unroll
+            for (int q = 0; q < NCU; ++q) {
+                double bt = RH[(size_t)j * NCU + q];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) bt = fma(gh[l * GH + NX + 1 + q], tv[l], bt);
+                acc = fma(Kj[q * PS + i], bt, acc);
+            }
+            L.dxv[e] = acc;
+        }
+        WSYNC();
+        // C3: p_j = vt_j + A^_j,x^T p_{j+1}: [p_j; 1] = M_j [p_{j+1}; 1], M_j = [[A^_j,x^T, vt_j], [0, 1]],
+        // the entries of A^_j,x^T formed from G^_j and K^_j a block ahead
+        {
+            const Mfma4Lane q = mfma4_lane(lane);
+            const bool lda = q.row < NX && q.col < NX, ldv = q.row < NX && q.col == NX;
+            const bool one = q.row == NX && q.col == NX;
+            // A^[col][row]: row `col` of G^, column `row` of K^
+            const double* gr = L.Gh + ((size_t)(HB - 1) * NX + (lda ? q.col : 0)) * GH;
+            const double* kc = L.K + (size_t)(HB - 1) * NCU * PS + (lda ? q.row : 0);
+            const int gcol = lda ? q.row : 0;
+            const int gs = lda ? NX * GH : 0, ks = lda ? NCU * PS : 0;
+            const double* vp = L.dxv + (size_t)(HB - 1) * NX + (ldv ? q.row : 0);
+            const int vs = ldv ? NX : 0;
+            if (lane < NX) L.P[(size_t)HB * PP + PO + lane] = L.gq[H * NB + lane];
+            double y = mfma4_vec(q, [&](int i) { return L.gq[H * NB + i]; });
+            const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+            const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+            double* out = stlo ? L.P + (size_t)(HB - 1) * PP + PO + q.r
+                               : (sthi ? L.P + (size_t)(HB - 1) * PP + PO + 4 + q.r : L.dummy + lane);
+            const int ost = (stlo || sthi) ? PP : 0;
+            CondOp o0, o1;
+            double v0, v1;
+            cond_op_load(gr, kc, gcol, o0);
+            v0 = *vp;
+            auto step = [&](const CondOp& op, double vv) {
+                const double a = lda ? cond_op(op) : (ldv ? vv : (one ? 1.0 : 0.0));
+                double sv;
+                y = mfma4_stage(a, y, sv);
+                *out = sv;
+                out -= ost;
+            };
+            int j = HB - 1;
+            for (; j >= 1; j -= 2) {
+                gr -= gs; kc -= ks; vp -= vs;
+                cond_op_load(gr, kc, gcol, o1);
+                v1 = *vp;
+                step(o0, v0);
+                if (j >= 2) {
+                    gr -= gs; kc -= ks; vp -= vs;
+                    cond_op_load(gr, kc, gcol, o0);
+                    v0 = *vp;
+                }
+                step(o1, v1);
+            }
+            if (j == 0) step(o0, v0);
+        }
+        WSYNC();
+        // C4: kff^_j = -Ru_j^-1 (r^_j + G^_u^T (t_j + p_{j+1}))
+        for (int e = lane; e < HB * NCU; e += 64) {
+            const int j = e / NCU, a = e - j * NCU;
+            const double* gh = L.Gh + (size_t)j * NX * GH;
+            const double* pn = L.P + (size_t)(j + 1) * PP + PO;
+            double wv[NX];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) wv[l] = L.Tc[(size_t)j * NX + l] + pn[l];
+            double kf = 0.0;
+#pragma unroll
+            for (int b2 = 0; b2 < NCU; ++b2) {
+                double acc = RH[(size_t)j * NCU + b2];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(gh[l * GH + NX + 1 + b2], wv[l], acc);
+                kf = fma(L.Rui[(size_t)j * NCU * NCU + a * NCU + b2], acc, kf);
+            }
+            L.K[(size_t)j * NCU * PS + a * PS + NX] = -kf;
+        }
+        WSYNC();
     }
 
     // ------------------------------------------------------------------ Riccati on MFMA, NX <= 12, NU <= 4
@@ -1503,8 +1503,7 @@ struct SqpKernel {
     //   Ru = M22 (readlane), Ru^-1 by 2x2 blocks (two reciprocals), K' = -Ru^-1 M21 per lane from the
     //   four u rows of its column (permlane16/32 swaps), P'_k = M11 + M21^T K' (one MFMA).
     // M21's element 0 (lane (a, j) = M21[a][j]) is both the Schur product's A operand and the
-    // right-hand side of K'.  Replaces the VALU riccati_factor (LDS round trips per product) for
-    // quad3d; outputs in its format (packed P', K', Ru^-1).
+    // right-hand side of K'.  Outputs as mfma_backward_h (packed P', K', Ru^-1).
     static constexpr bool kMfmaBig = !kMfma && NX <= 12 && NX + 1 <= 16 && NU == 4;
     __device__ static bool mfma_backward_big(const Lds& L, int H, int lane) {
         if constexpr (!kMfmaBig) {
@@ -1765,10 +1764,9 @@ struct SqpKernel {
     // Forward sweep: dx_0 = 0, dx_{k+1} = A'_k [dx_k; 1]  (M_k = [A'_k; e_NX]).  Masked lanes read the
     // LDS zero slot (stride 0) and the homogeneous corner the one slot, so the stage operand is one
     // unconditional load issued a stage ahead.
-    template <int VAR = 0>
     __device__ static void mfma4_forward(const Lds& L, int H, int lane) {
         static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
-        if constexpr (VAR == 0) {
+        {
             const Mfma4Lane q = mfma4_lane(lane);
             const bool ld = q.row < NX && q.col <= NX;
             const double* src = ld ? L.Acl + q.row * PS + q.col : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0);
@@ -1789,149 +1787,16 @@ struct SqpKernel {
                 *out = s;
                 out += ost;
             }
-        } else {
-            // two chained MFMAs per stage: block b computes row block (b & 1) of M_k y over the two
-            // K blocks, so D lands as (y'_lo, y'_hi, y'_lo, y'_hi); the next B operands are y_lo and
-            // y_hi in every block (two bank-masked DPP moves, independent of each other)
-            const int r = lane >> 4, b = (lane >> 2) & 3, c = lane & 3;
-            const int row = ((b & 1) ? 4 : 0) + c;
-            const bool l1 = row < NX && r <= NX, l2 = row < NX && 4 + r <= NX;
-            const double* s1 = l1 ? L.Acl + row * PS + r : L.zero + ((row == NX && r == NX) ? 7 : 0);
-            const double* s2 = l2 ? L.Acl + row * PS + 4 + r : L.zero + ((row == NX && 4 + r == NX) ? 7 : 0);
-            const int st1 = l1 ? NX * PS : 0, st2 = l2 ? NX * PS : 0;
-            const bool stlo = b == 0 && c == 0 && r < NX;
-            const bool sthi = b == 1 && c == 0 && 4 + r < NX;
-            double* out = stlo ? L.dxv + NX + r : (sthi ? L.dxv + NX + 4 + r : L.dummy + lane);
-            const int ost = (stlo || sthi) ? NX : 0;
-            if (lane < NX) L.dxv[lane] = 0.0;
-            double ylo = 0.0, yhi = (4 + r == NX) ? 1.0 : 0.0;
-            double a1n = *s1, a2n = *s2;
-            for (int k = 0; k < H; ++k) {
-                const double a1 = a1n, a2 = a2n;
-                s1 += (k + 1 < H) ? st1 : 0;
-                s2 += (k + 1 < H) ? st2 : 0;
-                a1n = *s1;
-                a2n = *s2;
-                double d = __builtin_amdgcn_mfma_f64_4x4x4f64(a1, ylo, 0.0, 0, 0, 0);
-                d = __builtin_amdgcn_mfma_f64_4x4x4f64(a2, yhi, d, 0, 0, 0);
-                *out = d;
-                out += ost;
-                ylo = dpp_merge<0x124, 0xA>(d, d);   // quads 1, 3 <- quads 0, 2 (row_ror:4)
-                yhi = dpp_merge<0x12C, 0x5>(d, d);   // quads 0, 2 <- quads 1, 3 (row_ror:12)
-            }
         }
-    }
-
-    // ---------------------------------------------------------------- DPP-free 4-block sweeps
-    // y_{k+1} = M_k y_k over the homogeneous 8-vector with no VALU on the recursion: the state is
-    // kept twice, yA (slots 0,1: y_lo, slots 2,3: y_hi) and yB (halves swapped), and a stage is four
-    // v_mfma_f64_4x4x4_4b, two accumulation chains of two:
-    //   A: slot half h computes y'_h = M_{h,h} y_h   (B = yA in place) + M_{h,1-h} y_{1-h}   (B = yB)
-    //   B: slot half h computes y'_{1-h} = M_{1-h,1-h} y_{1-h} (B = yB) + M_{1-h,h} y_h     (B = yA)
-    // so both outputs land exactly in the B layout of the next stage (result -> B operand and
-    // accumulator chains only).  Lane (r, b, c) supplies A_b[m = c][k = r] = M[4I + c][4J + r].
-    // `mget(k, row, col)` streams: a per-lane (pointer, stride) for each of the four blocks.
-    struct Sweep4 {
-        const double* p[4];
-        int st[4];
-    };
-    // blocks (I, J) of instructions 1A, 2A, 1B, 2B for slot half h
-    __device__ static void sweep4_blocks(int h, int (&I)[4], int (&J)[4]) {
-        I[0] = h;     J[0] = h;
-        I[1] = h;     J[1] = 1 - h;
-        I[2] = 1 - h; J[2] = 1 - h;
-        I[3] = 1 - h; J[3] = h;
-    }
-    template <int DIR>
-    __device__ static void sweep4_run(Sweep4& sw, int H, double yA, double yB, double* out, int ost) {
-        double an[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) an[q] = *sw.p[q];
-        for (int k = 0; k < H; ++k) {
-            double a[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                a[q] = an[q];
-                sw.p[q] += (k + 1 < H) ? DIR * sw.st[q] : 0;
-                an[q] = *sw.p[q];
-            }
-            const double t1 = __builtin_amdgcn_mfma_f64_4x4x4f64(a[0], yA, 0.0, 0, 0, 0);
-            const double t2 = __builtin_amdgcn_mfma_f64_4x4x4f64(a[2], yB, 0.0, 0, 0, 0);
-            const double nA = __builtin_amdgcn_mfma_f64_4x4x4f64(a[1], yB, t1, 0, 0, 0);
-            const double nB = __builtin_amdgcn_mfma_f64_4x4x4f64(a[3], yA, t2, 0, 0, 0);
-            yA = nA;
-            yB = nB;
-            *out = yA;
-            out += DIR * ost;
-        }
-    }
-
-    // Forward sweep dx_{k+1} = A'_k [dx_k; 1] (M_k = [A'_k; e_NX]) on the DPP-free scheme.
-    __device__ static void mfma4_forward2(const Lds& L, int H, int lane) {
-        static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
-        const int r = lane >> 4, c = lane & 3, b = (lane >> 2) & 3, h = b >> 1;
-        int I[4], J[4];
-        sweep4_blocks(h, I, J);
-        Sweep4 sw;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int row = 4 * I[q] + c, col = 4 * J[q] + r;
-            const bool ld = row < NX && col <= NX;
-            sw.p[q] = ld ? L.Acl + row * PS + col : L.zero + ((row == NX && col == NX) ? 7 : 0);
-            sw.st[q] = ld ? NX * PS : 0;
-        }
-        // y_0 = [0; 1; 0]: half h's entry r (index 4h + r)
-        const double yA = (4 * h + r == NX) ? 1.0 : 0.0, yB = (4 * (1 - h) + r == NX) ? 1.0 : 0.0;
-        const bool st = c == 0 && (b == 0 || b == 2) && 4 * h + r < NX;   // yA: slot 0 lo, slot 2 hi
-        double* out = st ? L.dxv + NX + 4 * h + r : L.dummy + lane;
-        if (lane < NX) L.dxv[lane] = 0.0;
-        sweep4_run<1>(sw, H, yA, yB, out, st ? NX : 0);
-    }
-
-    // Forward sweep on the VALU: dx_{k+1} = A'_k [dx_k; 1], lane i < NX owns dx[i] and the state
-    // is broadcast with v_readlane (scalar operands), so the chain has no MFMA output->operand
-    // latency and no LDS round trip; the rows of A'_{k+1} are fetched one stage ahead.
-    __device__ static void valu_forward(const Lds& L, int H, int lane) {
-        const int row = lane < NX ? lane : 0;
-        double x = 0.0;
-        if (lane < NX) L.dxv[lane] = 0.0;
-        double* out = (lane < NX) ? L.dxv + NX + lane : L.dummy + lane;
-        const int ost = (lane < NX) ? NX : 0;
-        const double* arow = L.Acl + row * PS;
-        auto load = [&](int k, double (&a)[PS]) {
-#pragma unroll
-            for (int j = 0; j < PS; ++j) a[j] = arow[(size_t)k * NX * PS + j];
-        };
-        auto step = [&](int k, const double (&a)[PS]) {
-            double acc0 = a[NX], acc1 = 0.0;
-#pragma unroll
-            for (int j = 0; j < NX; ++j) {
-                if (j & 1) acc1 = fma(a[j], readlane_d(x, j), acc1);
-                else acc0 = fma(a[j], readlane_d(x, j), acc0);
-            }
-            x = acc0 + acc1;
-            out[k * ost] = x;
-        };
-        double a0[PS], a1[PS];
-        load(0, a0);
-        int k = 0;
-        for (; k + 1 < H; k += 2) {
-            load(k + 1, a1);
-            step(k, a0);
-            if (k + 2 < H) load(k + 2, a0);
-            step(k + 1, a1);
-        }
-        if (k < H) step(k, a0);
     }
 
     // Corrector right-hand side with the factorisation unchanged (the Riccati "solve" of HPIPM):
     //   p_k = vt_k + A_cl,k^T p_{k+1},  vt_k = q_k + K_k^T r_k + A_cl,k^T P_{k+1} c_k,  p_H = q_H,
     //   kff_k = -Ru_k^-1 (r_k + B_k^T (P_{k+1} c_k + p_{k+1})),
-    // with [q; r] = gq.  Only the p recurrence is sequential (6-term VALU dot products with
-    // readlane broadcast); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
+    // with [q; r] = gq.  Only the p recurrence is sequential (one v_mfma_f64_4x4x4_4b + DPP merge per
+    // stage, mfma4_stage); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
-    template <int kMfma4 = 0>
-    __device__ static void valu_vector_backward(const Lds& L, int H, int lane) {
+    __device__ static void mfma4_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
         // entries (k, i) two per pass, both computed before either is stored (T and VT alias other
@@ -1973,29 +1838,7 @@ struct SqpKernel {
             if (has1) VT[e1] = a1;
         }
         WSYNC();
-        if constexpr (kMfma4 == 2) {
-            // p_k = vt_k + A'_k^T p_{k+1} on the DPP-free 4-block scheme (sweep4_run), stages H-1 .. 0:
-            // M_k = [[A'_k[:, :NX]^T, vt_k], [0, 1]], lane (r, b, c) supplies M[4I + c][4J + r]
-            const int r = lane >> 4, c = lane & 3, b = (lane >> 2) & 3, h = b >> 1;
-            int I[4], J[4];
-            sweep4_blocks(h, I, J);
-            Sweep4 sw;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = 4 * I[q] + c, col = 4 * J[q] + r;
-                const bool lda = row < NX && col < NX, ldv = row < NX && col == NX;
-                sw.p[q] = lda ? L.Acl + (size_t)(H - 1) * NX * PS + col * PS + row
-                              : (ldv ? VT + (size_t)(H - 1) * NX + row
-                                     : L.zero + ((row == NX && col == NX) ? 7 : 0));
-                sw.st[q] = lda ? NX * PS : (ldv ? NX : 0);
-            }
-            if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
-            auto yv = [&](int idx) { return idx < NX ? L.gq[H * NB + idx] : (idx == NX ? 1.0 : 0.0); };
-            const double yA = yv(4 * h + r), yB = yv(4 * (1 - h) + r);
-            const bool st = c == 0 && (b == 0 || b == 2) && 4 * h + r < NX;
-            double* out = st ? L.P + (size_t)(H - 1) * PP + PO + 4 * h + r : L.dummy + lane;
-            sweep4_run<-1>(sw, H, yA, yB, out, st ? PP : 0);
-        } else if constexpr (kMfma4 == 1) {
+        {
             // p_k = vt_k + A'_k^T p_{k+1} as the homogeneous recurrence [p_k; 1] = M_k [p_{k+1}; 1],
             // M_k = [[A'_k[:, :NX]^T, vt_k], [0, 1]] (mfma4_stage), stages H-1 .. 0
             const Mfma4Lane q = mfma4_lane(lane);
@@ -2021,39 +1864,6 @@ struct SqpKernel {
                 *out = sv;
                 out -= ost;
             }
-        } else {
-        const int col = lane < NX ? lane : 0;
-        double p = L.gq[H * NB + col];
-        if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
-        double* out = (lane < NX) ? L.P + PO + lane : L.dummy + lane;
-        const int ost = (lane < NX) ? PP : 0;
-        const double* acol = L.Acl + col;
-        struct Col { double a[NX]; double vt; };
-        auto load = [&](int k, Col& c) {
-#pragma unroll
-            for (int l = 0; l < NX; ++l) c.a[l] = acol[(size_t)k * NX * PS + l * PS];
-            c.vt = VT[k * NX + col];
-        };
-        auto step = [&](int k, const Col& c) {
-            double acc0 = c.vt, acc1 = 0.0;
-#pragma unroll
-            for (int l = 0; l < NX; ++l) {
-                if (l & 1) acc1 = fma(c.a[l], readlane_d(p, l), acc1);
-                else acc0 = fma(c.a[l], readlane_d(p, l), acc0);
-            }
-            p = acc0 + acc1;
-            out[k * ost] = p;
-        };
-        Col c0, c1;
-        load(H - 1, c0);
-        int k = H - 1;
-        for (; k >= 1; k -= 2) {
-            load(k - 1, c1);
-            step(k, c0);
-            if (k >= 2) load(k - 2, c0);
-            step(k - 1, c1);
-        }
-        if (k == 0) step(0, c0);
         }
         WSYNC();
         for (int e = lane; e < H * NU; e += 64) {
@@ -2128,26 +1938,6 @@ struct SqpKernel {
         }
     }
 
-    // dyn residual of stage k (lane < H): y_{k+1} - A_k y_k - B_k v_k - c_k for stage vectors y = [x; u]
-    __device__ static void dyn_residual(const Lds& L, int H, int lane, const double (&d)[NB], const double (&c)[NX],
-                                        double (&r)[NX]) {
-        double xn[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) xn[i] = __shfl(d[i], lane < 63 ? lane + 1 : 63);
-        const double* G = L.G + (size_t)min(lane, H - 1) * NX * GS;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double gr[NB];
-#pragma unroll
-            for (int j = 0; j < NB; ++j) gr[j] = G[i * GS + j];
-            double acc = xn[i] - c[i];
-#pragma unroll
-            for (int j = 0; j < NB; ++j) acc = fma(-gr[j], d[j], acc);
-            r[i] = (lane < H) ? acc : 0.0;
-        }
-    }
-
-
     // ------------------------------------------------------------------ IPM-layout helpers
     // (lane holds stage kq's variables vb .. vb + NV - 1; SPL: halves in lanes kq and kq + 32)
     // C' pi restricted to this lane's variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
@@ -2210,10 +2000,11 @@ struct SqpKernel {
     }
 
     // Step of stage kq from the Riccati solution, restricted to this lane's variables, and dpi_kq.
-    template <int NV>
+    template <int NV, int CF>
     __device__ static void recover_q(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
         double ddf[NB];
-        if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
+        if constexpr (CF == 2) recover_cond(L, H, kq, ddf, dp);
+        else if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
         else recover_step(L, H, kq, ddf, dp);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
@@ -2231,328 +2022,6 @@ struct SqpKernel {
         }
     }
 
-    // ------------------------------------------------------------------ Newton systems by cyclic reduction
-    // The IPM's Newton system  diag(h) dd + C' dp = -g,  C dd = c  (rows of C: dx_{k+1} - A_k dx_k -
-    // B_k du_k; c_k is column NB of G'_k) has a diagonal Hessian h (LINEAR_LS weights + barrier), so dd
-    // eliminates variable by variable and the dynamics multipliers pi = -dp solve the dual Schur
-    // complement, a block-tridiagonal SPD system of H blocks of NX:
-    //   Y_kk = G_k diag(ih_k) G_k' + diag(ihx_{k+1}),   Y_{k+1,k} = E_k = -A_{k+1} diag(ihx_{k+1}),
-    //   Y pi = rhs,  rhs_k = c_k + zx_{k+1} - G_k z_k,   ih = 1/h, z = ih g   (G_k = [A_k B_k];
-    //   ih = 0 for the fixed x_0 and the absent u_H),   dd = ih (C' pi - g).
-    // Odd-even cyclic reduction solves it in ceil(log2 H) levels, each parallel over its blocks
-    // (one lane per block or per block column), instead of H sequential Riccati stages: level l
-    // eliminates its odd blocks m with Cholesky factors L_m and X^l_m = L_m^-1 E_{m-1},
-    // X^r_m = L_m^-1 E_m' (one triangular solve per column), and updates the even ones,
-    //   D'_m = D_m - X^r_{m-1}' X^r_{m-1} - X^l_{m+1}' X^l_{m+1},   E'_m = -X^r_{m+1}' X^l_{m+1}.
-    // Storage: D (packed lower, Cholesky factors in place, 1/L_ii on the diagonal), the couplings of
-    // the levels >= 1 (level 0's come from G' and ih on the fly), the X blocks of the current level
-    // (they share their space with the solve's temporary vector) and the right-hand side, which the
-    // solve overwrites with pi.  (tools/cr_proto.py: same IPM iteration counts as the dense KKT.)
-    // Measured (tools/ab_variants.sh, quad2d H=30, B=1024): correct (every GPU parity test passes
-    // with it) but slower than the MFMA Riccati recursion -- SQP kernel 0.69 vs 0.38 ms: one wave
-    // issues an f64 op every ~5.5 cycles, and 6x6 blocks leave most lanes of a level idle, so the
-    // log-depth levels cost more than the 30 sequential 16x16x4 MFMA stages.  Opt-in: -DGPMPC_CR.
-#ifdef GPMPC_CR
-    static constexpr bool kCR = kMfma;
-#else
-    static constexpr bool kCR = false;
-#endif
-    static constexpr int TT = NX * (NX + 1) / 2, TB = NX * NX;
-    __host__ __device__ static constexpr int tri(int r, int c) { return r * (r + 1) / 2 + c; }
-    // blocks n and coupling offset eo (in blocks, levels >= 1) of level l; uniform scalar arithmetic
-    // (no per-level arrays: a runtime-indexed private array would live in scratch memory)
-    __host__ __device__ static void cr_level(int H, int l, int& n, int& eo) {
-        n = H;
-        eo = 0;
-        for (int q = 0; q < l; ++q) {
-            if (q >= 1) eo += n - 1;
-            n -= n >> 1;
-        }
-    }
-    __host__ __device__ static int cr_nlev(int H) {
-        int l = 0;
-        for (int n = H; n > 1; n -= n >> 1) ++l;
-        return l;
-    }
-    __host__ __device__ static size_t cr_eb_blocks(int H) {
-        size_t s = 0;
-        int n = H;
-        while (n > 1) {
-            n -= n >> 1;
-            s += (size_t)(n - 1);
-        }
-        return s;
-    }
-    __host__ __device__ static size_t cr_region(int H) {
-        const size_t xt = (size_t)2 * (H / 2) * TB, tv = (size_t)H * NX;
-        return (size_t)H * TT + cr_eb_blocks(H) * TB + (xt > tv ? xt : tv) + (size_t)H * NX;
-    }
-
-    // coupling E_m = Y_{m+1,m} of level l, entry (r, c)
-    __device__ static double cr_e(const Lds& L, int l, int eo, int m, int r, int c) {
-        if (l == 0) return -L.G[(size_t)(m + 1) * NX * GS + r * GS + c] * L.hq[(m + 1) * NB + c];
-        return L.Eb[(size_t)(eo + m) * TB + c * NX + r];
-    }
-    // b <- L^-1 b (packed lower factor, reciprocal diagonal)
-    __device__ static void cr_lsolve(const double* f, double (&b)[NX]) {
-        double a[TT];
-#pragma unroll
-        for (int q = 0; q < TT; ++q) a[q] = f[q];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) {
-            double acc = b[r];
-#pragma unroll
-            for (int k = 0; k < r; ++k) acc = fma(-a[tri(r, k)], b[k], acc);
-            b[r] = acc * a[tri(r, r)];
-        }
-    }
-    // b <- D^-1 b = L^-T L^-1 b
-    __device__ static void cr_dsolve(const double* f, double (&b)[NX]) {
-        double a[TT];
-#pragma unroll
-        for (int q = 0; q < TT; ++q) a[q] = f[q];
-#pragma unroll
-        for (int r = 0; r < NX; ++r) {
-            double acc = b[r];
-#pragma unroll
-            for (int k = 0; k < r; ++k) acc = fma(-a[tri(r, k)], b[k], acc);
-            b[r] = acc * a[tri(r, r)];
-        }
-#pragma unroll
-        for (int r = NX - 1; r >= 0; --r) {
-            double acc = b[r];
-#pragma unroll
-            for (int k = r + 1; k < NX; ++k) acc = fma(-a[tri(k, r)], b[k], acc);
-            b[r] = acc * a[tri(r, r)];
-        }
-    }
-    // in-place Cholesky of a packed SPD block: L (lower), 1/L_ii on the diagonal
-    __device__ static bool cr_chol(double* f) {
-        double a[TT];
-#pragma unroll
-        for (int q = 0; q < TT; ++q) a[q] = f[q];
-        bool ok = true;
-#pragma unroll
-        for (int c = 0; c < NX; ++c) {
-            double d = a[tri(c, c)];
-#pragma unroll
-            for (int k = 0; k < c; ++k) d = fma(-a[tri(c, k)], a[tri(c, k)], d);
-            ok = ok && (d > 0.0);
-            const double is = fast_rcp(__builtin_sqrt(d));
-            a[tri(c, c)] = is;
-#pragma unroll
-            for (int r = c + 1; r < NX; ++r) {
-                double v = a[tri(r, c)];
-#pragma unroll
-                for (int k = 0; k < c; ++k) v = fma(-a[tri(r, k)], a[tri(c, k)], v);
-                a[tri(r, c)] = v * is;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < TT; ++q) f[q] = a[q];
-        return ok;
-    }
-
-    // Y's diagonal blocks (packed lower), one lane per block column
-    __device__ static void cr_build(const Lds& L, int H, int lane) {
-        for (int t = lane; t < H * NX; t += 64) {
-            const int k = t / NX, c = t - k * NX;
-            const double* Gk = L.G + (size_t)k * NX * GS;
-            const double* ih = L.hq + k * NB;
-            double wv[NB];
-#pragma unroll
-            for (int v = 0; v < NB; ++v) wv[v] = Gk[c * GS + v] * ih[v];
-            const double dn = L.hq[(k + 1) * NB + c];
-            double* D = L.Dp + (size_t)k * TT;
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                if (r < c) continue;
-                double acc = (r == c) ? dn : 0.0;
-#pragma unroll
-                for (int v = 0; v < NB; ++v) acc = fma(Gk[r * GS + v], wv[v], acc);
-                D[tri(r, c)] = acc;
-            }
-        }
-    }
-
-    __device__ static bool cr_factor(const Lds& L, int H, int lane) {
-        bool ok = true;
-        int n = H, eo = 0, eon = 0;   // level l: blocks, coupling offsets of levels l and l + 1
-        for (int l = 0; n > 1; ++l) {
-            const int ne = n >> 1, ns = n - ne;
-            // F1: Cholesky of the odd blocks
-            for (int e = lane; e < ne; e += 64) ok = cr_chol(L.Dp + (size_t)((2 * e + 1) << l) * TT) && ok;
-            WSYNC();
-            // F2: X^l_m (columns q < NX) and X^r_m (q >= NX) of the odd blocks m = 2e + 1
-            for (int t = lane; t < ne * 2 * NX; t += 64) {
-                const int e = t / (2 * NX), q = t - e * 2 * NX, m = 2 * e + 1;
-                const bool right = q >= NX;
-                const int c = right ? q - NX : q;
-                if (right && m + 1 >= n) continue;
-                double bv[NX];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) bv[r] = right ? cr_e(L, l, eo, m, c, r) : cr_e(L, l, eo, m - 1, r, c);
-                cr_lsolve(L.Dp + (size_t)(m << l) * TT, bv);
-                double* X = L.XT + (size_t)(2 * e + (right ? 1 : 0)) * TB + c * NX;
-#pragma unroll
-                for (int r = 0; r < NX; ++r) X[r] = bv[r];
-            }
-            WSYNC();
-            // F3: D' of the even blocks (one lane per column) and the couplings of level l + 1
-            for (int t = lane; t < ns * NX; t += 64) {
-                const int s = t / NX, c = t - s * NX, m = 2 * s;
-                const bool hl = s >= 1, hr = m + 1 < n;
-                const double* Xa = L.XT + (size_t)(2 * (hl ? s - 1 : 0) + 1) * TB;   // X^r_{m-1}
-                const double* Xb = L.XT + (size_t)(2 * (hr ? s : 0)) * TB;            // X^l_{m+1}
-                double xa[NX], xb[NX];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) {
-                    xa[j] = hl ? Xa[c * NX + j] : 0.0;
-                    xb[j] = hr ? Xb[c * NX + j] : 0.0;
-                }
-                double* D = L.Dp + (size_t)(m << l) * TT;
-#pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    if (r < c) continue;
-                    double acc = D[tri(r, c)];
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) acc = fma(-(hl ? Xa[r * NX + j] : 0.0), xa[j], acc);
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) acc = fma(-(hr ? Xb[r * NX + j] : 0.0), xb[j], acc);
-                    D[tri(r, c)] = acc;
-                }
-            }
-            const int nc = ns - 1;   // couplings of level l + 1
-            for (int t = lane; t < nc * NX; t += 64) {
-                const int s = t / NX, c = t - s * NX;
-                const double* Xr = L.XT + (size_t)(2 * s + 1) * TB;
-                const double* Xl = L.XT + (size_t)(2 * s) * TB;
-                double xl[NX];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) xl[j] = Xl[c * NX + j];
-                double* Eo = L.Eb + (size_t)(eon + s) * TB + c * NX;
-#pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    double acc = 0.0;
-#pragma unroll
-                    for (int j = 0; j < NX; ++j) acc = fma(-Xr[r * NX + j], xl[j], acc);
-                    Eo[r] = acc;
-                }
-            }
-            WSYNC();
-            eo = eon;
-            eon += nc;
-            n = ns;
-        }
-        if (lane == 0) ok = cr_chol(L.Dp) && ok;   // the last block (original index 0)
-        WSYNC();
-        return wave_max(ok ? 0.0 : 1.0) == 0.0;
-    }
-
-    // right-hand side rhs_k = c_k + zx_{k+1} - G_k z_k of the current gq
-    __device__ static void cr_rhs(const Lds& L, int H, int lane) {
-        for (int t = lane; t < H * NX; t += 64) {
-            const int k = t / NX, i = t - k * NX;
-            const double* Gr = L.G + (size_t)k * NX * GS + i * GS;
-            double acc = fma(L.gq[(k + 1) * NB + i], L.hq[(k + 1) * NB + i], Gr[NB]);
-#pragma unroll
-            for (int v = 0; v < NB; ++v) acc = fma(-Gr[v], L.gq[k * NB + v] * L.hq[k * NB + v], acc);
-            L.RV[t] = acc;
-        }
-    }
-
-    // Y pi = rhs (in RV), pi overwrites RV
-    __device__ static void cr_solve(const Lds& L, int H, int lane) {
-        double* RV = L.RV;
-        double* TV = L.XT;
-        const int nlev = cr_nlev(H);
-        for (int l = 0; l < nlev; ++l) {
-            int n, eo;
-            cr_level(H, l, n, eo);
-            const int ne = n >> 1, ns = n - ne;
-            for (int e = lane; e < ne; e += 64) {   // t_m = D_m^-1 r_m
-                const int o = (2 * e + 1) << l;
-                double bv[NX];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) bv[r] = RV[o * NX + r];
-                cr_dsolve(L.Dp + (size_t)o * TT, bv);
-#pragma unroll
-                for (int r = 0; r < NX; ++r) TV[o * NX + r] = bv[r];
-            }
-            WSYNC();
-            for (int t = lane; t < ns * NX; t += 64) {   // r_m -= E_{m-1} t_{m-1} + E_m' t_{m+1}
-                const int s = t / NX, r = t - s * NX, m = 2 * s;
-                double acc = RV[(m << l) * NX + r];
-                if (s >= 1) {
-                    const double* tm = TV + ((m - 1) << l) * NX;
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m - 1, r, c), tm[c], acc);
-                }
-                if (m + 1 < n) {
-                    const double* tp = TV + ((m + 1) << l) * NX;
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m, c, r), tp[c], acc);
-                }
-                RV[(m << l) * NX + r] = acc;
-            }
-            WSYNC();
-        }
-        if (lane == 0) {
-            double bv[NX];
-#pragma unroll
-            for (int r = 0; r < NX; ++r) bv[r] = RV[r];
-            cr_dsolve(L.Dp, bv);
-#pragma unroll
-            for (int r = 0; r < NX; ++r) RV[r] = bv[r];
-        }
-        WSYNC();
-        for (int l = nlev - 1; l >= 0; --l) {
-            int n, eo;
-            cr_level(H, l, n, eo);
-            const int ne = n >> 1;
-            for (int t = lane; t < ne * NX; t += 64) {   // v_m = r_m - E_{m-1} pi_{m-1} - E_m' pi_{m+1}
-                const int e = t / NX, r = t - e * NX, m = 2 * e + 1;
-                double acc = RV[(m << l) * NX + r];
-                const double* pm = RV + ((m - 1) << l) * NX;
-#pragma unroll
-                for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m - 1, r, c), pm[c], acc);
-                if (m + 1 < n) {
-                    const double* pp = RV + ((m + 1) << l) * NX;
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) acc = fma(-cr_e(L, l, eo, m, c, r), pp[c], acc);
-                }
-                TV[(m << l) * NX + r] = acc;
-            }
-            WSYNC();
-            for (int e = lane; e < ne; e += 64) {   // pi_m = D_m^-1 v_m
-                const int o = (2 * e + 1) << l;
-                double bv[NX];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) bv[r] = TV[o * NX + r];
-                cr_dsolve(L.Dp + (size_t)o * TT, bv);
-#pragma unroll
-                for (int r = 0; r < NX; ++r) RV[o * NX + r] = bv[r];
-            }
-            WSYNC();
-        }
-    }
-
-    // dp_kq = -pi_kq and this lane's step dd = ih (C' pi - g) = -ih (g + C' dp)
-    template <bool SPL, int NV>
-    __device__ static void recover_cr(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
-#pragma unroll
-        for (int i = 0; i < NX; ++i) dp[i] = (kq < H) ? -L.RV[min(kq, H - 1) * NX + i] : 0.0;
-        double ctq[NV];
-        ctpi_q<SPL, NV>(L, H, kq, vb, dp, ctq);
-        const int kk = min(kq, H);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const int v = vb + j;
-            const bool av = v < NX ? (kq >= 1 && kq <= H) : (v < NB && kq < H);
-            dd[j] = av ? -(L.gq[kk * NB + v] + ctq[j]) * L.hq[kk * NB + v] : 0.0;
-        }
-    }
-
     // ------------------------------------------------------------------ the QP (HPIPM's role), Mehrotra IPM
     // IPM layout: lane l holds stage kq's variables v = vb + j (j < NV).  SPL: the stage vectors are
     // split over lanes kq and kq + 32 (NV = NB/2), halving the per-lane IPM state and the elementwise
@@ -2562,10 +2031,14 @@ struct SqpKernel {
     // NV variables' IPM state (the unsplit layout spilled 3.5 KB per lane to scratch at H = 40).  The
     // full step vector for the dynamics residual, the reductions and the Riccati status cross the
     // waves through LDS at block barriers; the Riccati recursion runs on wave 0.
-    static constexpr bool WSPL = NWAVES > 1;
-    static_assert(!WSPL || NB % NWAVES == 0, "WSPL: whole variables per wave");
+    // (the single-tile models keep their two-lanes-per-stage split on wave 0 when they run four waves:
+    // their helpers take the GP tile passes only -- sharing the IPM's elementwise work costs more in
+    // cross-wave reductions than it saves at NB <= 8)
+    static constexpr bool WSPL = NWAVES > 1 && !kMfma;
+    // (WSPL: NWAVES NV may exceed NB -- cartpole's 5 variables in slots of 2 -- and the slots past NB
+    // are inactive: never stored, never published)
     template <bool SPL>
-    __host__ __device__ static constexpr int nv_of() { return WSPL ? NB / NWAVES : (SPL ? (NB + 1) / 2 : NB); }
+    __host__ __device__ static constexpr int nv_of() { return WSPL ? (NB + NWAVES - 1) / NWAVES : (SPL ? (NB + 1) / 2 : NB); }
     struct Tm {   // phase-timing state (GPMPC_TIMING)
         unsigned long long acc[kPhases];
         unsigned long long last;
@@ -2623,7 +2096,8 @@ struct SqpKernel {
         if constexpr (WSPL) {
             if (kq <= H) {
 #pragma unroll
-                for (int j = 0; j < NV; ++j) L.Dq[(size_t)kq * NB + vb + j] = d[j];
+                for (int j = 0; j < NV; ++j)
+                    if (vb + j < NB) L.Dq[(size_t)kq * NB + vb + j] = d[j];
             }
             __syncthreads();
             const double* dk = L.Dq + (size_t)min(kq, H) * NB;
@@ -2659,7 +2133,7 @@ struct SqpKernel {
         const int kk = min(lane, H), vb = wv * NV;
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            const int v = vb + j;
+            const int v = vb + j < NB ? vb + j : NB - 1;   // (slots past NB: inactive, any finite value)
             blo[j] = L.hq[(size_t)kk * NB + v];
             bup[j] = L.gq[(size_t)kk * NB + v];
             gv[j] = L.Dq[(size_t)kk * NB + v];
@@ -2675,7 +2149,8 @@ struct SqpKernel {
     __device__ static void qp_publish_step(const Lds& L, int H, int lane, int wv, const double (&d)[NV]) {
         if (lane <= H) {
 #pragma unroll
-            for (int j = 0; j < NV; ++j) L.Dq[(size_t)lane * NB + wv * NV + j] = d[j];
+            for (int j = 0; j < NV; ++j)
+                if (wv * NV + j < NB) L.Dq[(size_t)lane * NB + wv * NV + j] = d[j];
         }
         __syncthreads();
     }
@@ -2683,8 +2158,8 @@ struct SqpKernel {
     // One QP of the SQP iteration: blo/bup/gv/hd/d (this lane's variables) and cqq (the stage's
     // dynamics residual) in, the step d, the bound multipliers and piq (dynamics multipliers of
     // stage kq) out.  Every wave of the instance calls it (WSPL) with the same control flow.
-    template <bool SPL, int NV>
-    __device__ static bool qp_ipm(const ProblemDev& P, const StateDev& S, int b, const Lds& L, int H, int lane, int wv, const Entries& E,
+    template <bool SPL, int NV, int CF>
+    __device__ static bool qp_ipm(const ProblemDev& P, const Lds& L, int H, int lane, int wv,
                                   const double (&blo)[NV], const double (&bup)[NV], const double (&gv)[NV],
                                   const double (&hd)[NV], double (&d)[NV], const double (&cqq)[NX], double (&ll)[NV],
                                   double (&lu)[NV], double (&piq)[NX], int& qit_out, Tm& tm) {
@@ -2705,46 +2180,8 @@ struct SqpKernel {
         (void)tm;
 #endif
         double sl[NV], su[NV];
-#ifndef GPMPC_QP_WARM_PIQ
-#define GPMPC_QP_WARM_PIQ 1
-#endif
-#if defined(GPMPC_QP_WARM_PI)
-        // experiment: only the dynamics multipliers warm-started, bound multipliers and slacks cold
-#pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const bool av = avq(j);
-            sl[j] = av ? fmax(-blo[j], 1e-2) : 1.0;
-            su[j] = av ? fmax(bup[j], 1e-2) : 1.0;
-            ll[j] = av ? P.qp_mu0 * fast_rcp(sl[j]) : 0.0;
-            lu[j] = av ? P.qp_mu0 * fast_rcp(su[j]) : 0.0;
-        }
-        {
-            const double* pq = S.pi + ((size_t)b * H + min(kq, H - 1)) * NX;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) piq[i] = actu_q ? pq[i] : 0.0;
-        }
-#elif defined(GPMPC_QP_WARM)
-        // warm start (acados qp_solver_warm_start-like; experiment): slacks at the current bound
-        // distances, bound and dynamics multipliers from the last QP solution (acados memory),
-        // all floored at GPMPC_QP_WARM
-        {
-            const double fl = GPMPC_QP_WARM;
-            const double* lq = S.lam + ((size_t)b * (H + 1) + k_q) * 2 * NB + vb;
-#pragma unroll
-            for (int j = 0; j < NV; ++j) {
-                const bool av = avq(j);
-                sl[j] = av ? fmax(-blo[j], fl) : 1.0;
-                su[j] = av ? fmax(bup[j], fl) : 1.0;
-                ll[j] = av ? fmax(lq[j < NB - vb ? j : 0], fl) : 0.0;
-                lu[j] = av ? fmax(lq[NB + (j < NB - vb ? j : 0)], fl) : 0.0;
-            }
-            const double* pq = S.pi + ((size_t)b * H + min(kq, H - 1)) * NX;
-#pragma unroll
-            for (int i = 0; i < NX; ++i) piq[i] = (actu_q && GPMPC_QP_WARM_PIQ) ? pq[i] : 0.0;
-        }
-#else
-        (void)S;
-        (void)b;
+        // cold start (acados / HPIPM default): slacks at the bound distances floored at 1e-2,
+        // multipliers mu0 / s, dynamics multipliers 0
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const bool av = avq(j);
@@ -2755,7 +2192,10 @@ struct SqpKernel {
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) piq[i] = 0.0;
-#endif
+        if constexpr (CF == 2) {   // G^_x, G^_u of this SQP iteration's linearisation
+            if (wv == 0) cond_ghat<true>(L, H, lane);
+            WSYNC();
+        }
         bool qp_ok = true;
         int qit = 0, par = 0;
         TPHASE(3);
@@ -2787,9 +2227,9 @@ struct SqpKernel {
                     if (on_q && vb + j < NB) {
                         // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
                         const double hv = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
-                        if constexpr (kCR) L.hq[k_q * NB + vb + j] = av ? fast_rcp(hv) : 0.0;   // ih = 1/h
-                        else L.hq[k_q * NB + vb + j] = hv;
-                        L.gq[k_q * NB + vb + j] = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
+                        const double gqv = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
+                        L.hq[k_q * NB + vb + j] = hv;
+                        L.gq[k_q * NB + vb + j] = gqv;
                     }
                 }
 #pragma unroll
@@ -2808,59 +2248,50 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(4);
                 double dd[NV], dp[NX];
-                if constexpr (kCR) {
-                    cr_build(L, H, lane);
-                    WSYNC();
-                    if (!cr_factor(L, H, lane)) { qp_ok = false; break; }
-                    TPHASE(6);
-                    cr_rhs(L, H, lane);
-                    WSYNC();
-                    cr_solve(L, H, lane);
-                    TPHASE(9);
-                    recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
-                    TPHASE(3);
-                } else if constexpr (kMfma) {
+                if constexpr (kMfma) {
                     bool rok = true;
                     if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
-                        rok = mfma_backward_h(L, H, lane);
-                        WSYNC();
-                        TPHASE(8);
-                        if (rok) acl_phase<true>(L, H, lane);
-                        WSYNC();
-                        TPHASE(6);
-                        if (rok) {
-#ifdef GPMPC_SWEEP_VALU
-                            valu_forward(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                            mfma4_forward2(L, H, lane);
-#else
-                            mfma4_forward(L, H, lane);
-#endif
+                        if constexpr (CF == 2) {
+                            cond_ghat<false>(L, H, lane);   // c^ of the current dynamics residual
+                            WSYNC();
+                            TPHASE(4);
+                            rok = cond_backward(L, H, lane);
+                            WSYNC();
+                            TPHASE(6);
+                            if (rok) cond_forward(L, H, lane);
+                            WSYNC();
+                            TPHASE(9);
+                            if (rok) cond_expand(L, H, lane);
+                        } else {
+                            rok = mfma_backward_h(L, H, lane);
+                            WSYNC();
+                            TPHASE(8);
+                            if (rok) acl_phase<true>(L, H, lane);
+                            WSYNC();
+                            TPHASE(6);
+                            if (rok) mfma4_forward(L, H, lane);
                         }
                         WSYNC();
                     }
                     if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
-                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else {
                     // the recursion on wave 0 (WSPL: the other waves wait at the status exchange)
+                    static_assert(kMfmaBig, "stage products must fit one (mfma_backward_h) or two (mfma_backward_big) tiles");
                     bool rok = true;
                     if (wv == 0) {
-                        if constexpr (kMfmaBig) {
-                            rok = mfma_backward_big(L, H, lane);
-                            WSYNC();
-                        } else {
-                            rok = riccati_factor(L, H, lane, E);
-                        }
+                        rok = mfma_backward_big(L, H, lane);
+                        WSYNC();
                         TPHASE(6);
-                        if (rok) forward_big(L, H, lane);
+                        if (rok) valu_forward_big(L, H, lane);
                     }
                     if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(3);
-                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
                 }
                 // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
                 // alpha_max = 1 / max(1, max_i -dv_i / v_i)
@@ -2905,48 +2336,38 @@ struct SqpKernel {
                 }
                 XSYNC();
                 TPHASE(5);
-                if constexpr (kCR) {
-                    cr_rhs(L, H, lane);
-                    WSYNC();
-                    cr_solve(L, H, lane);
-                    TPHASE(9);
-                    recover_cr<SPL, NV>(L, H, kq, vb, dd, dp);
-                    TPHASE(3);
-                } else if constexpr (kMfma) {
+                if constexpr (kMfma) {
                     if (wv == 0) {
-#ifdef GPMPC_SWEEP_VALU
-                        valu_vector_backward<0>(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                        valu_vector_backward<2>(L, H, lane);
-#else
-                        valu_vector_backward<1>(L, H, lane);
-#endif
-                        TPHASE(8);
-                        acl_phase<false>(L, H, lane);
-                        WSYNC();
-                        TPHASE(6);
-#ifdef GPMPC_SWEEP_VALU
-                        valu_forward(L, H, lane);
-#elif defined(GPMPC_SWEEP4)
-                        mfma4_forward2(L, H, lane);
-#else
-                        mfma4_forward(L, H, lane);
-#endif
+                        if constexpr (CF == 2) {
+                            cond_vector_backward(L, H, lane);
+                            TPHASE(6);
+                            cond_forward(L, H, lane);
+                            WSYNC();
+                            TPHASE(9);
+                            cond_expand(L, H, lane);
+                        } else {
+                            mfma4_vector_backward(L, H, lane);
+                            TPHASE(8);
+                            acl_phase<false>(L, H, lane);
+                            WSYNC();
+                            TPHASE(6);
+                            mfma4_forward(L, H, lane);
+                        }
                         WSYNC();
                     }
                     XSYNC();
                     TPHASE(9);
-                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else {
                     if (wv == 0) {
-                        vector_big(L, H, lane);
+                        valu_vector_big(L, H, lane);
                         TPHASE(6);
-                        forward_big(L, H, lane);
+                        valu_forward_big(L, H, lane);
                     }
                     XSYNC();
                     TPHASE(3);
-                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
                 }
                 rmax = 1.0;
                 double dsl[NV], dsu[NV], dll[NV], dlu[NV];
@@ -3002,6 +2423,7 @@ struct SqpKernel {
     // ends the loop with command -1 at the end of the kernel (one more B1).
     // Command -2 (WSPL): the wave takes its variables' share of the QP (qp_ipm) and publishes its
     // part of the step at B2.
+    template <int CF>
     __device__ static void helper_loop(const ProblemDev& P, const StateDev& S, const Lds& L, int w, int lane, int b) {
         const int H = P.H;
         const int ne = (H + 15) >> 4, np = 16 * ne;
@@ -3016,16 +2438,18 @@ struct SqpKernel {
                     qp_setup_pub<NV>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq);
                     Tm tm{};
                     int qit = 0;
-                    const bool ok = qp_ipm<false, NV>(P, S, b, L, H, lane, w, decode(lane), blo, bup, gv, hd, d, cqq, ll, lu,
-                                                      piq, qit, tm);
+                    const bool ok = qp_ipm<false, NV, CF>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
                     if (ok && lane <= H) {   // this wave's bound multipliers (acados memory)
-                        double* lam_q = S.lam + ((size_t)b * (H + 1) + lane) * 2 * NB;
+                        double* lam_q = lds_mult(CF) ? L.lam + (size_t)lane * 2 * NB
+                                                     : S.lam + ((size_t)b * (H + 1) + lane) * 2 * NB;
 #pragma unroll
                         for (int j = 0; j < NV; ++j) {
                             const int v = w * NV + j;
                             const bool ab = v < NX ? (lane >= 1) : (lane < H);
-                            lam_q[v] = ab ? ll[j] : 0.0;
-                            lam_q[NB + v] = ab ? lu[j] : 0.0;
+                            if (v < NB) {
+                                lam_q[v] = ab ? ll[j] : 0.0;
+                                lam_q[NB + v] = ab ? lu[j] : 0.0;
+                            }
                         }
                     }
                     qp_publish_step<NV>(L, H, lane, w, d);   // B2
@@ -3045,16 +2469,17 @@ struct SqpKernel {
 
     // ------------------------------------------------------------------ the kernel body
     // SPL: the QP's per-variable state is split over two lanes per stage (needs H + 1 <= 32)
-    template <bool SPL>
+    // CF: stages per block of the Newton-system recursions (2: condensed, needs kCond and H even)
+    template <bool SPL, int CF>
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
         const int lane = threadIdx.x & 63;
         const int b = blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
-        const Lds L = carve(smem, H);
+        const Lds L = carve<CF>(smem, H);
         if constexpr (NWAVES > 1) {
             if (threadIdx.x >= 64) {   // GP helper wave
-                helper_loop(P, S, L, threadIdx.x >> 6, lane, b);
+                helper_loop<CF>(P, S, L, threadIdx.x >> 6, lane, b);
                 return;
             }
         }
@@ -3083,15 +2508,31 @@ struct SqpKernel {
         tcur = 7;
 #endif
         // ---------------- load instance state (acados memory: iterate + multipliers)
-        // The multipliers stay in global memory (this lane's rows of S.lam / S.pi): they are read
-        // once per SQP iteration for the residuals and written after each QP, so they hold no
-        // registers through the QP (the register file is the binding resource of this kernel).
+        // The multipliers are read once per SQP iteration for the residuals and written after each
+        // QP, so they hold no registers through the QP (the register file is the binding resource of
+        // this kernel): they live in LDS during the step (this lane's rows of L.lam / L.pim) and go
+        // to global memory (S.lam / S.pi) once, at the end of the step, when the layout has room
+        // (lds_mult); otherwise every SQP iteration reads and writes the global rows.
+        constexpr bool kLM = lds_mult(CF);
         double w[NB];
         const double* xg = S.x + (size_t)b * (H + 1) * NX;
         const double* ug = S.u + (size_t)b * H * NU;
         double* lam_g = S.lam + ((size_t)b * (H + 1) + k) * 2 * NB;
         double* pi_g = S.pi + ((size_t)b * H + (act_u ? k : 0)) * NX;
-        double* lam_q = S.lam + ((size_t)b * (H + 1) + k_q) * 2 * NB;   // this lane's stage in the IPM layout
+        double* lam_l = kLM ? L.lam + (size_t)k * 2 * NB : lam_g;          // this lane's stage
+        double* pi_l = kLM ? L.pim + (size_t)(act_u ? k : 0) * NX : pi_g;
+        double* lam_q = kLM ? L.lam + (size_t)k_q * 2 * NB                  // this lane's stage in the IPM layout
+                            : S.lam + ((size_t)b * (H + 1) + k_q) * 2 * NB;
+        if constexpr (kLM) {
+            if (on) {
+#pragma unroll
+                for (int v = 0; v < 2 * NB; ++v) lam_l[v] = lam_g[v];
+            }
+            if (act_u) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) pi_l[i] = pi_g[i];
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NX; ++i) w[i] = on ? xg[k * NX + i] : 0.0;
 #pragma unroll
@@ -3172,7 +2613,6 @@ struct SqpKernel {
         auto lbv = [&](int v) { return (v < NX ? P.x_lo[v] : P.u_lo[v - NX]) + tsd[v] - P.uh; };
         auto ubv = [&](int v) { return (v < NX ? P.x_hi[v] : P.u_hi[v - NX]) - tsd[v] + P.uh; };
 
-        [[maybe_unused]] const Entries E = decode(lane);
         // ---------------- stage-0 state rows (gpmpc.py:288,296,309-310; mpc.py:141,145,157-158)
         // x_0 is pinned to obs (lbx = ubx = obs, gpmpc.py:339-340), so these rows only decide
         // feasibility: an obs outside the stage-0 box by more than the inequality tolerance makes
@@ -3212,11 +2652,11 @@ struct SqpKernel {
 #pragma unroll
             for (int v = 0; v < NB; ++v) {
                 const bool av = v < NX ? act_x : act_u;
-                lamL[v] = av ? lam_g[v] : 0.0;
-                lamU[v] = av ? lam_g[NB + v] : 0.0;
+                lamL[v] = av ? lam_l[v] : 0.0;
+                lamU[v] = av ? lam_l[NB + v] : 0.0;
             }
 #pragma unroll
-            for (int i = 0; i < NX; ++i) pi[i] = act_u ? pi_g[i] : 0.0;
+            for (int i = 0; i < NX; ++i) pi[i] = act_u ? pi_l[i] : 0.0;
             double F[NX];
             TPHASE(1);
 #ifdef GPMPC_TIMING
@@ -3343,7 +2783,7 @@ struct SqpKernel {
                 }
             }
             int qit = 0;
-            const bool qp_ok = qp_ipm<SPL, NV>(P, S, b, L, H, lane, 0, E, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
+            const bool qp_ok = qp_ipm<SPL, NV, CF>(P, L, H, lane, 0, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
             if constexpr (WSPL) qp_publish_step<NV>(L, H, lane, 0, d);   // B2: the full step in Dq
             qp_total += qit;
             TPHASE(2);
@@ -3375,7 +2815,7 @@ struct SqpKernel {
             }
             if (act_u) {
 #pragma unroll
-                for (int i = 0; i < NX; ++i) pi_g[i] = piq[i];
+                for (int i = 0; i < NX; ++i) pi_l[i] = piq[i];
             }
             if (lane == 0) {
 #pragma unroll
@@ -3396,14 +2836,23 @@ struct SqpKernel {
         // restart from zero, u0 is the previous solution's first input and the next step runs
         // untightened (as after a reset).
         const bool good = (status == kSuccess) || (status == kMaxIter);
-        if (good) {   // (the multipliers are already in S.lam / S.pi)
+        if constexpr (kLM) WSYNC();   // the last QP's multiplier rows (both lanes of a split stage) are in LDS
+        if (good) {
             if (on) {
 #pragma unroll
                 for (int i = 0; i < NX; ++i) xo[k * NX + i] = w[i];
+                if constexpr (kLM) {
+#pragma unroll
+                    for (int v = 0; v < 2 * NB; ++v) lam_g[v] = lam_l[v];
+                }
             }
             if (act_u) {
 #pragma unroll
                 for (int a = 0; a < NU; ++a) uo[k * NU + a] = w[NX + a];
+                if constexpr (kLM) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) pi_g[i] = pi_l[i];
+                }
             }
         } else {
             if (on) {
@@ -3475,36 +2924,57 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
     return hipGetLastError();
 }
 
-// One wave per SIMD (the instance owns the register file), except the two-wave quad2d variant
-// (GPMPC_W2), which must fit two waves per SIMD.
-template <int ID>
-constexpr int kWavesPerEU = (SqpKernel<ID>::NWAVES == 2) ? 2 : 1;
-template <int ID, bool SPL>
-__global__ __launch_bounds__(64 * SqpKernel<ID>::NWAVES) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<ID>, kWavesPerEU<ID>))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
-    SqpKernel<ID>::template run<SPL>(P, S, io);
+// One wave per SIMD: every wave of an instance owns a SIMD's register file.
+template <int ID, int NW, bool SPL, int CF>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
+    SqpKernel<ID, NW>::template run<SPL, CF>(P, S, io);
 }
 
-template <int ID, bool SPL>
+template <int ID, int NW, bool SPL, int CF>
 hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
-    const size_t lds = SqpKernel<ID>::lds_doubles(P.H) * sizeof(double);
+    const size_t lds = SqpKernel<ID, NW>::lds_doubles(P.H, CF) * sizeof(double);
     if (lds > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, SPL>,
+        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL, CF>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((sqp_step_kernel<ID, SPL>), dim3(batch), dim3(64 * SqpKernel<ID>::NWAVES), lds, stream, P, S, io);
+    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, CF>), dim3(batch), dim3(64 * NW), lds, stream, P, S, io);
     return hipGetLastError();
+}
+
+template <int ID, int NW, bool SPL>
+hipError_t launch_sqp_cf(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+    using K = SqpKernel<ID, NW>;
+    if constexpr (K::kCond) {
+        if (P.condense && K::cf_of(P.H) == 2) return launch_sqp_variant<ID, NW, SPL, 2>(P, S, io, batch, stream);
+    }
+    return launch_sqp_variant<ID, NW, SPL, 1>(P, S, io, batch, stream);
+}
+
+// waves per instance for this launch: the model's default, or (single-tile models) four when every
+// instance can have a CU of its own (batch <= CUs) and the request allows it (P.waves: 0 = auto)
+template <int ID>
+int sqp_waves(const ProblemDev& P, int batch) {
+    if constexpr (kDefaultWaves<ID> > 1) {
+        return kDefaultWaves<ID>;
+    } else {
+        if (P.waves == 1 || P.waves == 4) return P.waves;
+        return (P.n_cu > 0 && batch <= P.n_cu) ? 4 : 1;
+    }
 }
 
 template <int ID>
 hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
-    // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
-    // (multi-wave models split the IPM state over their waves instead: WSPL)
-#ifndef GPMPC_NO_SPLIT
-    if constexpr (SqpKernel<ID>::NWAVES == 1)
-        if (P.H + 1 <= 32) return launch_sqp_variant<ID, true>(P, S, io, batch, stream);
-#endif
-    return launch_sqp_variant<ID, false>(P, S, io, batch, stream);
+    if constexpr (kDefaultWaves<ID> == 1) {
+        // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
+        const bool spl = P.H + 1 <= 32;
+        if (sqp_waves<ID>(P, batch) == 4)
+            return spl ? launch_sqp_cf<ID, 4, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 4, false>(P, S, io, batch, stream);
+        return spl ? launch_sqp_cf<ID, 1, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 1, false>(P, S, io, batch, stream);
+    } else {
+        // multi-wave models split the IPM state over their waves instead (WSPL)
+        return launch_sqp_cf<ID, kDefaultWaves<ID>, false>(P, S, io, batch, stream);
+    }
 }
 
 template <int ID>
@@ -3522,11 +2992,18 @@ int model_unc_dims(int model, int32_t* unc) {
     return 0;
 }
 
+template <int ID>
+static size_t lds_bytes_of(int H) {   // the larger of the default-wave layouts a launch may pick
+    using K = SqpKernel<ID>;
+    const size_t a = K::lds_doubles(H, 1), b = K::lds_doubles(H, K::cf_of(H));
+    return (a > b ? a : b) * sizeof(double);
+}
+
 size_t sqp_lds_bytes(int model, int H) {
     switch (model) {
-        case kQuad2D: return SqpKernel<kQuad2D>::lds_doubles(H) * sizeof(double);
-        case kQuad3D: return SqpKernel<kQuad3D>::lds_doubles(H) * sizeof(double);
-        case kCartpole: return SqpKernel<kCartpole>::lds_doubles(H) * sizeof(double);
+        case kQuad2D: return lds_bytes_of<kQuad2D>(H);
+        case kQuad3D: return lds_bytes_of<kQuad3D>(H);
+        case kCartpole: return lds_bytes_of<kCartpole>(H);
     }
     return 0;
 }

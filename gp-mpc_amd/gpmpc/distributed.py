@@ -28,6 +28,17 @@ def shard_range(batch_per_rank: int, rank: int) -> range:
     return range(rank * batch_per_rank, (rank + 1) * batch_per_rank)
 
 
+def shard_slice(global_batch: int, rank: int, world: int) -> range:
+    """Global instance ids owned by ``rank`` when ``global_batch`` instances are split over
+    ``world`` ranks (strong scaling, SURVEY.md §8(e) "contiguous B/G slices"): contiguous slices
+    whose sizes differ by at most one, every instance on exactly one rank."""
+    if global_batch < world:
+        raise ValueError(f"global batch {global_batch} < {world} ranks")
+    base, extra = divmod(global_batch, world)
+    start = rank * base + min(rank, extra)
+    return range(start, start + base + (1 if rank < extra else 0))
+
+
 def replicate_training_data(data: list[tuple[np.ndarray, np.ndarray]], device=None) -> list[tuple[np.ndarray, np.ndarray]]:
     """Broadcast every GP's (X, y) from rank 0 so all replicas are identical."""
     rank, size = world()

@@ -121,6 +121,7 @@ class BatchSolver:
         if variance not in ("exact", "love"):
             raise ValueError("variance must be 'exact' or 'love'")
         self.love_ranks = [None] * self.spec.n_gp   # columns of each GP's LOVE root (None: exact)
+        self.love_roots = [None] * self.spec.n_gp   # the uploaded roots (host, float64), for checkers
         if gps is None:
             _lib.check(self.lib.gpmpc_use_gp(self._h, 0))
             self.gps = None
@@ -145,6 +146,7 @@ class BatchSolver:
                 R = _c(gp.love_root(love_rank).cpu().numpy())
                 _lib.check(self.lib.gpmpc_set_gp_variance_root(self._h, g, R.shape[0], R.shape[1], R.ctypes.data))
                 self.love_ranks[g] = R.shape[1]
+                self.love_roots[g] = R
         _lib.check(self.lib.gpmpc_use_gp(self._h, 1))
         self.gps = gps
 
@@ -184,6 +186,11 @@ class BatchSolver:
             assert buf.shape == (self.batch, self.STATS_SLOTS) and buf.dtype == torch.int64 and buf.device == self.device
         self._stats = buf
         _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr(), self.STATS_SLOTS))
+
+    def set_launch(self, waves: int = 0, condense: bool = False):
+        """SQP-kernel launch shape (gpmpc_set_launch): waves per instance (0 auto, 1, 4) and the
+        condensed stage-pair recursions.  Performance options; results agree to rounding."""
+        _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves), int(bool(condense))))
 
     def set_profiling(self, enabled: bool):
         _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))

@@ -169,6 +169,16 @@ gpmpc_status gpmpc_gp_posterior(int32_t n, int32_t d, int32_t npad, const double
 gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* params, const double* x,
                               const double* u, double* x_next, int32_t* tstep, void* stream);
 
+/* Launch shape of the SQP kernel (no reference counterpart: the reference solves one instance).
+ *   waves     0 = auto: one wavefront per instance, or -- for the models whose stage fits one MFMA
+ *             tile (quad2d, cartpole) -- four per instance when batch <= the device's compute units,
+ *             so the SIMDs that would idle take the GP tile sums and the IPM's elementwise work;
+ *             1 / 4 force either (quad3d always runs four).
+ *   condense  1 = the Newton systems' Riccati recursions run over condensed stage pairs when H is
+ *             even (single-tile models), 0 (default) = stage by stage.
+ * Results are identical up to floating-point rounding; both are performance options. */
+gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves, int32_t condense);
+
 /* Kernel timing with HIP events recorded on the solve stream around the variance kernel
  * and the SQP kernel of every gpmpc_solve while enabled.  gpmpc_kernel_times synchronises
  * on the recorded events, returns the summed milliseconds and launch counts, and clears them.

@@ -37,6 +37,24 @@ def test_self_launch_two_ranks_shards_and_max_timing():
     assert abs(out["value"] - 2 * B * steps / (out["ms_per_step"] * 1e-3 * steps)) <= 1e-6 * out["value"]
 
 
+def test_global_batch_strong_scaling_slices():
+    """--global-batch G: contiguous B/G slices (sizes differing by at most one) covering every
+    instance once; the job value counts G instances, scaling "strong"."""
+    G, steps = 9, 4
+    out = _run(["--gpus", "2", "--dry-run", "--global-batch", str(G), "--steps", str(steps), "--warmup", "0"])
+    assert out["scaling"] == "strong" and out["config"]["global_batch"] == G
+    assert [s[:2] for s in out["shards"]] == [[0, 5], [5, 9]]
+    assert abs(out["value"] - G * steps / (out["ms_per_step"] * 1e-3 * steps)) <= 1e-6 * out["value"]
+    sys.path.insert(0, str(ROOT / "gp-mpc_amd"))
+    from gpmpc import distributed as D
+
+    for g, w in ((1024, 8), (1024, 3), (7, 7), (100, 6)):
+        sl = [D.shard_slice(g, r, w) for r in range(w)]
+        assert sl[0].start == 0 and sl[-1].stop == g
+        assert all(a.stop == b.start for a, b in zip(sl, sl[1:]))
+        assert max(len(x) for x in sl) - min(len(x) for x in sl) <= 1
+
+
 def test_single_rank_needs_no_launcher():
     out = _run(["--gpus", "1", "--dry-run", "--batch", "4", "--steps", "2", "--warmup", "0"])
     assert out["n_gpus"] == 1 and out["shards"] == [[0, 4, out["shards"][0][2]]]
@@ -75,6 +93,7 @@ def test_bench_line_contract_on_the_gpu():
     assert 1.0 <= out["linearisations_per_step"] <= out["sqp_iter_mean"] + 1.0
     cb = out["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference")
+    assert cb["window"] == [1, 4] and cb["sqp_iter_mean"] > 0   # the GPU leg's own timed window
 
 
 def test_flop_counts_match_survey_8d():

@@ -1,0 +1,74 @@
+"""Launch shapes of the SQP kernel give the same solutions (MI355X only).
+
+gpmpc_set_launch picks, per call, one wavefront or four per instance (four when the batch leaves
+SIMDs idle: the helper waves take the GP tile sums and the IPM's elementwise work) and the
+two-stage condensed Riccati recursions (H even).  Every combination is run here on the same closed
+loop against the C++ restatement (oracle/cpu_ref.cpp) at KKT tolerance 1e-9: identical status,
+|x_gpu - x_cpu| and |u_gpu - u_cpu| <= 1e-6 (1 + |.|).  H = 15 is odd: no condensing there.
+"""
+
+import numpy as np
+import pytest
+
+from helpers import O, initial_states, lqr, oracle_gps, problem, product_gps
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.parametrize("waves,condense", [(1, 0), (1, 1), (4, 0), (4, 1)])
+@pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 12, 4), ("cartpole", 50, 20, 12, 4),
+                                               ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
+def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, condense):
+    torch = _torch()
+    from oracle import cpu_ref
+    from gpmpc.solver import BatchSolver
+
+    if not cpu_ref.LIB_PATH.exists():
+        pytest.skip("oracle/lib/libcpuref.so not built")
+    spec, data, hyp = problem(name, N)
+    gpo, gpp = oracle_gps(data, hyp), product_gps(data, hyp)
+    mats = lqr(spec)
+    tol = 1e-9
+    ref = cpu_ref.CpuRef(spec, H, B, gps=gpo, lqr_mats=mats, tol=tol, qp_tol=1e-11, qp_max_iter=100)
+    gs = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)
+    gs.set_launch(waves=waves, condense=bool(condense))
+    gs.set_gps(gpp)
+    gs.set_tightening(True, 0.95, *mats)
+    gs.reset(reset_iterate=True)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, B)
+    plant = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
+    for s in range(steps):
+        gs.solve(torch.tensor(x0, device="cuda"), torch.tensor(phase + s, dtype=torch.int32, device="cuda"))
+        u0 = ref.step(x0, phase + s, threads=4).copy()
+        xg, ug, tg = (t.cpu().numpy() for t in gs.solution())
+        st = gs.status.cpu().numpy()
+        np.testing.assert_array_equal(st, ref.status)
+        ok = st == 0
+        assert ok.mean() >= 0.75, (s, st)
+        err = np.abs(xg - ref.x).max(axis=(1, 2)) / (1 + np.abs(ref.x).max(axis=(1, 2)))
+        assert err[ok].max() <= 1e-6, (s, err[ok].max())
+        eu = np.abs(ug - ref.u).max(axis=(1, 2)) / (1 + np.abs(ref.u).max(axis=(1, 2)))
+        assert eu[ok].max() <= 1e-6, (s, eu[ok].max())
+        for b in range(B):
+            x0[b] = plant.rk4(x0[b], u0[b])[0]
+
+
+def test_launch_option_validation():
+    _torch()
+    from gpmpc import _lib
+    from gpmpc.solver import BatchSolver
+
+    spec, _, _ = problem("quad2d", 20)
+    gs = BatchSolver(spec, 10, 2)
+    with pytest.raises(_lib.GPMPCError):
+        gs.set_launch(waves=2)
+    gs.set_launch(waves=0, condense=True)
