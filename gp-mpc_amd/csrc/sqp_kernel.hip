@@ -128,6 +128,16 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Branch-free per-lane select (v_bfi_b32 on both halves): m all ones -> a, zero -> b.  A ternary on
+// values computed only for the selecting lanes lets the compiler sink their computation into exec-
+// masked branches; the bit select needs both values on every lane.
+__device__ __forceinline__ double bsel(unsigned m, double a, double b) {
+    const unsigned long long ia = __double_as_longlong(a), ib = __double_as_longlong(b);
+    const unsigned lo = ((unsigned)ia & m) | ((unsigned)ib & ~m);
+    const unsigned hi = ((unsigned)(ia >> 32) & m) | ((unsigned)(ib >> 32) & ~m);
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
@@ -956,12 +966,12 @@ struct SqpKernel {
     // layout x_t (t < NX), CI = NX, u_k0 at UI .. UI+NU-1, u_k1 at UI+NU .. UI+NCU-1 (UI = 8).  With
     // T = [G'_k0; e_CI] (x_k1 = T z) and the condensed dynamics x_2j+2 = G^_j z,
     //   G^_j = A_k1 T + B_k1 (u_k1 slots) + c_k1 e_CI^T        (stored per block: [G^_x | c^ | G^_u]),
-    // the block's cost-to-go is  M = G^''^T P'_{j+1} G^'' + E^T E + D^  with
-    //   E (tile rows 8 + m, m < NX):  sqrt(h_m) T[m][.] + (g_m / sqrt(h_m)) e_CI^T   (h, g: hq, gq of x_k1),
-    // so E^T E = T^T diag(h) T plus the gradient terms in row/column CI (the (CI, CI) entry is a
+    // the block's cost-to-go is  M = G^''^T P'_{j+1} G^'' + E_A^T E_B + D^  with (tile rows 8 + m, m < NX)
+    //   E_A = diag(h) T + g e_CI^T,  E_B = T + diag(g / h) e_CI^T        (h, g: hq, gq of x_k1),
+    // so E_A^T E_B = T^T diag(h) T plus the gradient terms in row/column CI (the (CI, CI) entry is a
     // constant of the cost-to-go, never read), and D^ the diagonal / gradient of x_k0, u_k0, u_k1.
     // On v_mfma_f64_16x16x4: W = P' G^'' (2 MFMAs), M = G^''^T W over K-steps 0..1 on top of
-    // E^T E + D^ (K-steps 2..3, whose W rows are E itself: the identity block of the stacked system),
+    // E_A^T E_B + D^ (K-steps 2..3 of the stacked system [P' 0; 0 I], whose operands are E_A / E_B),
     // then Ru = M_uu (NCU x NCU), K^' = -Ru^-1 M_u and P'_j = M + M_.u K^' (1 MFMA) as in
     // mfma_backward_h: five dependent MFMA links per block instead of ten per stage pair.  The next
     // block's operands are 11 LDS loads issued behind the W products; its E^T E products run on the
@@ -1105,17 +1115,23 @@ struct SqpKernel {
                 pd[r] -= dst[r];
             }
         };
-        // E rows and E^T E + D^ (K-steps 2, 3 of M: independent of P')
-        auto make = [&](const Raw& rw, Blk& bk) {
-            double e[2];
+        // E_A, E_B rows (VALU) and E_A^T E_B + D^ (K-steps 2, 3 of M: independent of P', 2 MFMAs)
+        const unsigned mci = lc == CI ? ~0u : 0u;
+        struct Eop { double a[2], b[2], d[3]; };
+        auto make_e = [&](const Raw& rw, Blk& bk, Eop& eo) {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const double sh = __builtin_sqrt(rw.h[q]);
-                e[q] = fma(sh, rw.t[q], lc == CI ? rw.q[q] * fast_rcp(sh) : 0.0);
+                const double gi = rw.q[q] * fast_rcp(rw.h[q]);
+                eo.a[q] = fma(rw.h[q], rw.t[q], bsel(mci, rw.q[q], 0.0));
+                eo.b[q] = rw.t[q] + bsel(mci, gi, 0.0);
                 bk.g[q] = rw.g[q];
             }
-            bk.mb = mfma64(e[0], e[0], f64x4{rw.d[0], rw.d[1], rw.d[2], 0.0});
-            bk.mb = mfma64(e[1], e[1], bk.mb);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) eo.d[r] = rw.d[r];
+        };
+        auto make_mb = [&](const Eop& eo, Blk& bk) {
+            bk.mb = mfma64(eo.a[0], eo.b[0], f64x4{eo.d[0], eo.d[1], eo.d[2], 0.0});
+            bk.mb = mfma64(eo.a[1], eo.b[1], bk.mb);
         };
         // store streams (blocks HB-1 .. 0), dummy slot with stride 0 for entries not stored
         double* sp[2];
@@ -1147,9 +1163,16 @@ struct SqpKernel {
             *srui = pend_r;
             srui -= srui_st;
         };
-        // one block: the chain W -> M -> Ru^-1 -> Schur; the next block's loads behind W, its E^T E
-        // while the VALU forms Ru^-1
+        // one block: the chain W -> M -> Ru^-1 -> Schur.  The next block's loads are issued behind
+        // the W products, its E operands formed in the shadow of the M products, and its two
+        // E_A^T E_B MFMAs issued right after M (the matrix core idles while the VALU forms Ru^-1)
         Raw rw;
+        Eop eo;
+        const unsigned ma0 = lr == 0 ? ~0u : 0u, ma1 = lr == 1 ? ~0u : 0u, ma2 = lr == 2 ? ~0u : 0u;
+        const unsigned mb1 = (lr & 2) ? ~0u : 0u, mb2 = (lr & 1) ? ~0u : 0u, mb3 = ((lr ^ (lr >> 1)) & 1) ? ~0u : 0u;
+        const int tsel = lc ^ lr;
+        const unsigned mt0 = tsel == 0 ? ~0u : 0u, mt1 = tsel == 1 ? ~0u : 0u, mt2 = tsel == 2 ? ~0u : 0u;
+        const unsigned ml0 = lane == 0 ? ~0u : 0u, ml17 = lane == 17 ? ~0u : 0u, mlu = lr < NCU ? ~0u : 0u;
         auto block = [&](const Blk& cb, Blk& nb, bool more) {
             f64x4 w = mfma64(pn[0], cb.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
             w = mfma64(pn[1], cb.g[1], w);
@@ -1161,7 +1184,10 @@ struct SqpKernel {
             f64x4 m = mfma64(cb.g[0], w[0], cb.mb);
             m = mfma64(cb.g[1], w[1], m);
             __builtin_amdgcn_sched_barrier(0);
-            if (more) make(rw, nb);
+            if (more) {
+                make_e(rw, nb, eo);
+                make_mb(eo, nb);
+            }
             __builtin_amdgcn_sched_barrier(0);
             const double mu = m[2];          // lane (q, c) <- M[UI + q][c]
             double kb, rv;
@@ -1177,7 +1203,7 @@ struct SqpKernel {
                 const double t = num * -r0;
                 const double id = fma(r0, ee, r0);
                 kb = fma(t, ee, t);
-                rv = (lane == 0) ? r11 * id : ((lane == 17) ? r00 * id : -r01 * id);
+                rv = bsel(ml0, r11 * id, bsel(ml17, r00 * id, -r01 * id));
             } else {
                 // Ru^-1 by 2x2 blocks [[A, B], [B^T, C]] (as mfma_backward_big)
                 const double a00 = readlane_d(mu, UI), a01 = readlane_d(mu, UI + 1), a11 = readlane_d(mu, 16 + UI + 1);
@@ -1200,17 +1226,16 @@ struct SqpKernel {
                 const double Y10 = fma(X10, C00, X11 * C01), Y11 = fma(X10, C01, X11 * C11);
                 const double Z00 = A00 + fma(Y00, X00, Y01 * X01), Z01 = A01 + fma(Y00, X10, Y01 * X11);
                 const double Z11 = A11 + fma(Y10, X10, Y11 * X11);
-                const int a = lr;   // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a, column a ^ t
-                const double c0 = (a == 0) ? Z00 : ((a == 1) ? Z11 : ((a == 2) ? C00 : C11));
-                const double c1 = (a & 2) ? C01 : Z01;
-                const double c2 = (a & 1) ? -Y11 : -Y00;
-                const double c3 = ((a ^ (a >> 1)) & 1) ? -Y10 : -Y01;
+                // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a = lr, column a ^ t (branch-free lane selects)
+                const double c0 = bsel(ma0, Z00, bsel(ma1, Z11, bsel(ma2, C00, C11)));
+                const double c1 = bsel(mb1, C01, Z01);
+                const double c2 = bsel(mb2, -Y11, -Y00);
+                const double c3 = bsel(mb3, -Y10, -Y01);
                 const double v1 = xor16_d(mu), v2 = xor32_d(mu), v3 = xor32_d(v1);   // rows UI + (a ^ 1, 2, 3)
                 kb = -fma(c0, mu, fma(c1, v1, fma(c2, v2, c3 * v3)));
-                const int tt = lc ^ a;
-                rv = (tt == 0) ? c0 : ((tt == 1) ? c1 : ((tt == 2) ? c2 : c3));
+                rv = bsel(mt0, c0, bsel(mt1, c1, bsel(mt2, c2, c3)));
             }
-            const f64x4 pk = mfma64(lr < NCU ? mu : 0.0, kb, m);   // P'_j = M + M_.u K^'
+            const f64x4 pk = mfma64(bsel(mlu, mu, 0.0), kb, m);   // P'_j = M + M_.u K^'
             pend_p[0] = pk[0];
             pend_p[1] = pk[1];
             pend_k = kb;
@@ -1220,7 +1245,8 @@ struct SqpKernel {
         };
         Blk b0, b1;
         load(rw);
-        make(rw, b0);
+        make_e(rw, b0, eo);
+        make_mb(eo, b0);
         int j = HB - 1;
         for (; j >= 1; j -= 2) {   // two blocks per iteration (ping-pong: no register copies)
             block(b0, b1, true);
@@ -1592,6 +1618,10 @@ struct SqpKernel {
         const bool rst = lr < NU && lc < NU;
         double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lr * NU + lc : L.dummy + lane;
         const int srui_st = rst ? NU * NU : 0;
+        const unsigned ma0 = lr == 0 ? ~0u : 0u, ma1 = lr == 1 ? ~0u : 0u, ma2 = lr == 2 ? ~0u : 0u;
+        const unsigned mb1 = (lr & 2) ? ~0u : 0u, mb2 = (lr & 1) ? ~0u : 0u, mb3 = ((lr ^ (lr >> 1)) & 1) ? ~0u : 0u;
+        const int tsel = lc ^ lr;
+        const unsigned mt0 = tsel == 0 ? ~0u : 0u, mt1 = tsel == 1 ? ~0u : 0u, mt2 = tsel == 2 ? ~0u : 0u;
         auto stage = [&](const Stage& sd) {
             f64x4 w1 = {0.0, 0.0, 0.0, 0.0}, w2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1631,19 +1661,17 @@ struct SqpKernel {
             const double Y10 = fma(X10, C00, X11 * C01), Y11 = fma(X10, C01, X11 * C11);
             const double Z00 = A00 + fma(Y00, X00, Y01 * X01), Z01 = A01 + fma(Y00, X10, Y01 * X11);
             const double Z11 = A11 + fma(Y10, X10, Y11 * X11);
-            // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a, column a ^ t, for lane group a
-            const int a = lr;
-            const double c0 = (a == 0) ? Z00 : ((a == 1) ? Z11 : ((a == 2) ? C00 : C11));
-            const double c1 = (a & 2) ? C01 : Z01;
-            const double c2 = (a & 1) ? -Y11 : -Y00;                  // (0,2) = -Y00, (1,3) = -Y11
-            const double c3 = ((a ^ (a >> 1)) & 1) ? -Y10 : -Y01;    // (0,3) = -Y01, (1,2) = -Y10
+            // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a, column a ^ t, for lane group a (branch-free selects)
+            const double c0 = bsel(ma0, Z00, bsel(ma1, Z11, bsel(ma2, C00, C11)));
+            const double c1 = bsel(mb1, C01, Z01);
+            const double c2 = bsel(mb2, -Y11, -Y00);                  // (0,2) = -Y00, (1,3) = -Y11
+            const double c3 = bsel(mb3, -Y10, -Y01);                  // (0,3) = -Y01, (1,2) = -Y10
             // the four u rows of this lane's column of M21 (lane group b holds row b)
             const double v0 = m21[0], v1 = xor16_d(v0), v2 = xor32_d(v0), v3 = xor32_d(v1);
             const double kb = -fma(c0, v0, fma(c1, v1, fma(c2, v2, c3 * v3)));
             const f64x4 pk = mfma64(lr < NU ? v0 : 0.0, kb, m11);   // P'_k = M11 + M21^T K'
             // stores: P' (packed), K' (feedback + kff), Ru^-1 (lane (a, c): column c = a ^ t)
-            const int t = lc ^ a;
-            const double rv = (t == 0) ? c0 : ((t == 1) ? c1 : ((t == 2) ? c2 : c3));
+            const double rv = bsel(mt0, c0, bsel(mt1, c1, bsel(mt2, c2, c3)));
 #pragma unroll
             for (int r = 0; r < KS; ++r) {
                 *sp[r] = pk[r];
