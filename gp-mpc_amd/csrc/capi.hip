@@ -80,6 +80,7 @@ struct gpmpc_handle {
     int gp_npad[kMaxGP] = {0, 0, 0, 0};
     double* gp_vroot[kMaxGP] = {nullptr, nullptr, nullptr, nullptr};   // LOVE roots (tightening only)
     int gp_vroot_cols[kMaxGP] = {0, 0, 0, 0};
+    int gp_vroot_rank[kMaxGP] = {0, 0, 0, 0};
     // optional per-kernel HIP-event timing (bench.py's roofline leg)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -413,6 +414,7 @@ gpmpc_status gpmpc_set_gp_variance_root(gpmpc_handle* h, int32_t gp_id, int32_t 
     HIPCHK(hipMalloc(&h->gp_vroot[gp_id], rp.size() * sizeof(double)));
     HIPCHK(hipMemcpy(h->gp_vroot[gp_id], rp.data(), rp.size() * sizeof(double), hipMemcpyHostToDevice));
     h->gp_vroot_cols[gp_id] = rpad;
+    h->gp_vroot_rank[gp_id] = r;
     return GPMPC_OK;
 }
 
@@ -561,6 +563,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             pb.g[g] = P.gp[g];
             pb.g[g].vroot = h->gp_vroot[g];   // LOVE (fast_pred_var) when a root is set
             pb.g[g].vroot_cols = h->gp_vroot_cols[g];
+            pb.g[g].vroot_rank = h->gp_vroot_rank[g];
             pb.npad[g] = h->gp_npad[g];
         }
         HIPCHK(launch_gp_post_batch(pb, true, s));

@@ -289,19 +289,29 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
 }
 
 // ---------------------------------------------------------------------------- variance, LOVE root
-// var(z) = sf2 - ||R^T k(z, X)||^2 (+ sn2) with the dense LOVE root R [npad][16 NTC]
-// (gpytorch fast_pred_var; NTC = the widest root of the launch in 16-column tiles, 7 for the
-// rank-100 roots of configs 4/5): 2 N (16 NTC) flops per point on the matrix core against one exp
-// per training row.  No LDS and no barriers: one wavefront = 16
-// points, K-steps of four training rows (lane (kq, lc): point lc, row 4s + kq) on
-// v_mfma_f64_16x16x4_f64, four K-steps per round with their exps interleaved (exp_rbf_n) and the
-// next round's training rows and root entries loaded a round ahead (the blocks of one GP run
-// together, so its root, 3.6 MB at N = 4000 and 112 columns, streams through L2 once per wave
-// generation).  No 16-tile accumulator array and no LDS: the round-ahead loads hide the latency
-// (the two round buffers take 256 VGPRs + 18 AGPRs, one wave per SIMD; two waves per SIMD measured
-// slower), against one barrier per 16-row panel in gp_post_kernel.  sf2 is applied to the squared norm (sf2^2), not
-// to every kernel value.
+// var(z) = sf2 - ||R^T k(z, X)||^2 (+ sn2) with the dense LOVE root R [npad][rank, padded to 16]
+// (gpytorch fast_pred_var, rank <= 100 for configs 4/5).  No LDS and no barriers: one wavefront =
+// 16 points, K-steps of four training rows (lane (kq, lc): point lc, row 4s + kq), four K-steps per
+// round with their exps interleaved (exp_rbf_n) and the next round's training rows and root entries
+// loaded a round ahead (the blocks of one GP run together, so its root, 3.6 MB at N = 4000 and 112
+// columns, streams through L2 once per wave generation).  Per GP (love_tiles) the root's columns
+// go to nf full 16-column tiles on v_mfma_f64_16x16x4_f64 (accumulators acc[t]) and, when at most
+// 8 columns remain, nq <= 2 four-column quads on v_mfma_f64_4x4x4_4b_f64, whose A operand is the
+// same register (block b takes A_b[m][k] from lane 16k + 4b + m = point 4b + m, row k) and whose B
+// operand is the quad's four columns replicated over the blocks: D_b[m][n] (lane 16m + 4b + n) is
+// point 4b + m against column n, a quarter of a 16-column tile's matrix-core cycles for the last
+// 4 of a rank-100 root's columns (the tile would be 12/16 padding).  Each GP of the launch does
+// only its own tiles (the 12-column thrust root of config 4 one tile, not the pitch root's 7).
+// The two round buffers take the kernel to ~256 VGPRs, one wave per SIMD (two measured slower).
+// sf2 is applied to the squared norm (sf2^2), not to every kernel value.
 constexpr int kLoveWaves = 4;
+constexpr int kLoveMaxTiles = 8;
+__host__ __device__ inline void love_tiles(int rank, int& nf, int& nq) {
+    nf = rank >> 4;
+    const int rem = rank & 15;
+    nq = (rem + 3) >> 2;
+    if (nq > 2) { nf += 1; nq = 0; }
+}
 template <int NTC, bool FROM_STATE>
 __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) {
     const GPDev& g = pb.g[blockIdx.y];
@@ -316,22 +326,29 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
     load_point<FROM_STATE>(a, p < a.P ? p : a.P - 1, z);
     const double c = -0.5 * g.inv_ell2;
     const double4* rows = reinterpret_cast<const double4*>(g.vrows);
-    const int NC = g.vroot_cols, ntc = NC / 16;   // this GP's root width (<= 16 NTC)
-    const double* Rl = g.vroot + kq * NC + lc;   // this lane's B entries: R[16 s4 + 4 ks + kq][16 t + lc]
+    const int NC = g.vroot_cols;   // row stride of the padded root
+    int nf, nq;                    // this GP's full tiles (<= NTC) and four-column quads (<= 2)
+    love_tiles(g.vroot_rank, nf, nq);
+    const double* Rl = g.vroot + kq * NC + lc;                        // R[16 s4 + 4 ks + kq][16 t + lc]
+    const double* Rq = g.vroot + kq * NC + 16 * nf + (lc & 3);        // R[..][16 nf + 4 q + n]
     const int nv = g.nv, nround = npad / 16;
-    struct Round { double4 x[4]; double b[4][NTC]; };
+    struct Round { double4 x[4]; double b[4][NTC]; double bq[4][2]; };
     auto load = [&](int s4, Round& rd) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
             const int i = 16 * s4 + 4 * ks + kq;
             rd.x[ks] = rows[i < nv ? i : 0];
+            const size_t ro = (size_t)(16 * s4 + 4 * ks) * NC;
 #pragma unroll
-            for (int t = 0; t < NTC; ++t) rd.b[ks][t] = (t < ntc) ? Rl[(size_t)(16 * s4 + 4 * ks) * NC + 16 * t] : 0.0;
+            for (int t = 0; t < NTC; ++t) rd.b[ks][t] = (t < nf) ? Rl[ro + 16 * t] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) rd.bq[ks][q] = (q < nq) ? Rq[ro + 4 * q] : 0.0;
         }
     };
     f64x4 acc[NTC];
 #pragma unroll
     for (int t = 0; t < NTC; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double accq[2] = {0.0, 0.0};
     auto round = [&](int s4, const Round& rd) {
         double kv[4];
 #pragma unroll
@@ -345,7 +362,11 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
         for (int ks = 0; ks < 4; ++ks) {
             const double kvm = (16 * s4 + 4 * ks + kq < nv) ? kv[ks] : 0.0;
 #pragma unroll
-            for (int t = 0; t < NTC; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kvm, rd.b[ks][t], acc[t], 0, 0, 0);
+            for (int t = 0; t < NTC; ++t)
+                if (t < nf) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kvm, rd.b[ks][t], acc[t], 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (q < nq) accq[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(kvm, rd.bq[ks][q], accq[q], 0, 0, 0);
         }
     };
     // (measured on configs 4/5: this plain form beats unconditional clamped prefetches, with or
@@ -360,7 +381,12 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
         round(s4 + 1, r1);
     }
     if (s4 < nround) round(s4, r0);
-    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+    // acc[t][r]: point kq + 4r, column 16 t + lc; accq[q] (lane 16 m + 4 b + n): point 4 b + m,
+    // column 16 nf + 4 q + n, i.e. row kq's point kq + 4r sits in the lanes of quad r
+    const double tq = fma(accq[0], accq[0], accq[1] * accq[1]);
+    double sq[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sq[r] = ((lc >> 2) == r) ? tq : 0.0;
 #pragma unroll
     for (int t = 0; t < NTC; ++t)
 #pragma unroll
@@ -379,7 +405,7 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
 
 template <bool FROM_STATE, int NTC = 1>
 hipError_t launch_love(const PostBatch& pb, int ntc, hipStream_t stream) {
-    if constexpr (NTC <= 8) {
+    if constexpr (NTC <= kLoveMaxTiles) {
         if (ntc == NTC) {
             int blocks = 0;
             for (int q = 0; q < pb.n; ++q) blocks = max(blocks, (pb.a[q].P + 16 * kLoveWaves - 1) / (16 * kLoveWaves));
@@ -424,14 +450,17 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
     bool love = true;   // every entry variance-only with a LOVE root of <= 128 columns
-    int wmax = 0;
+    int tmax = 1;       // the launch's widest full-tile count (love_tiles)
     for (int q = 0; q < pb.n; ++q) {
         love = love && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].vroot != nullptr &&
-               pb.g[q].vroot_cols % 16 == 0 && pb.g[q].vroot_cols <= 128;
-        wmax = max(wmax, pb.g[q].vroot_cols);
+               pb.g[q].vroot_cols % 16 == 0 && pb.g[q].vroot_cols <= 16 * kLoveMaxTiles &&
+               pb.g[q].vroot_rank >= 1 && pb.g[q].vroot_rank <= pb.g[q].vroot_cols;
+        int nf = 0, nq = 0;
+        love_tiles(pb.g[q].vroot_rank, nf, nq);
+        tmax = max(tmax, nf);
     }
     if (love)
-        return from_state ? launch_love<true>(pb, wmax / 16, stream) : launch_love<false>(pb, wmax / 16, stream);
+        return from_state ? launch_love<true>(pb, tmax, stream) : launch_love<false>(pb, tmax, stream);
     bool tri = true;   // every entry variance-only with the same npad <= 256
     for (int q = 0; q < pb.n; ++q)
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&

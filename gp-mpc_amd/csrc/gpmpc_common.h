@@ -41,7 +41,8 @@ struct GPDev {
     // R R^T ~ (K + sn2 I)^-1; when set, the variance is sf2 - ||R^T k||^2 instead of the exact
     // triangular form (set only in the tightening's variance launch).  NULL: exact.
     const double* vroot;
-    int32_t vroot_cols;
+    int32_t vroot_cols;   // padded to 16
+    int32_t vroot_rank;   // the root's columns before padding
     double inv_ell2;      // 1 / lengthscale^2 (isotropic RBF, gpmpc/gp.py:34)
     double sf2;           // outputscale
     double sn2;           // likelihood noise (gpmpc/gp.py:31)

@@ -302,9 +302,11 @@ struct SqpKernel {
     static constexpr bool kCond = kMfma && NCU <= 4;
     // stages per block of the Newton-system recursions for horizon H (1: stage by stage)
     __host__ __device__ static constexpr int cf_of(int H) { return (kCond && H % 2 == 0) ? 2 : 1; }
-    // multipliers kept in LDS during the step (the layouts with room for them: condensed blocks or
-    // one instance per CU); otherwise they stay in global memory (rows read / written per SQP iteration)
-    __host__ __device__ static constexpr bool lds_mult(int CF) { return NW > 1; }
+    // multipliers kept in LDS during the step when the layout has room for them (single-tile models on
+    // four waves: one instance per CU); otherwise they stay in global memory (rows read / written per
+    // SQP iteration).  quad3d keeps them global: its LDS copy measured 4.6 % slower at config 5 (the
+    // 14 KB push its 140 KB layout further and the copies sit on the step's critical path).
+    __host__ __device__ static constexpr bool lds_mult(int CF) { return NW > 1 && kMfma; }
     static constexpr int GH = NX + 1 + NCU;   // row of the condensed dynamics G^_j: [G^_x | c^ | G^_u]
     // Waves per instance.  The wide model (quad3d) needs more LDS than two instances per CU can
     // have, so its CU's other SIMDs would idle: three GP helper waves take a share of every GP
@@ -318,7 +320,7 @@ struct SqpKernel {
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
-        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *cd, *Sig, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
+        double *G, *P, *K, *Rui, *hq, *gq, *dxv, *cd, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
         double *Dq, *xs;             // WSPL: step-vector exchange, reduction slots
         double *Gh, *dpv, *Tc;       // condensed blocks (CF = 2): G^_j rows, dpi of every stage (and
                                      // the corrector's block gradients), corrector scratch t_j
@@ -326,7 +328,8 @@ struct SqpKernel {
                                      // bounds [H+1][2 NB], dynamics [H][NX]
         int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
-    __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC + 2 * NX * NX + NU * NX; }
+    // tightening: per-stage noise terms cd_k of the covariance convolution
+    __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC; }
     // GP evaluation scratch of the linearisation: points [NGP][16*NE][4], c|z|^2 [NGP][16*NE], sums
     // [NGP][16*NE][4].  It aliases
     // the P' region, which is dead between the QP solves.
@@ -396,7 +399,6 @@ struct SqpKernel {
             L.Acl = s;
             L.Gh = s;
             L.cd = s;
-            L.Sig = s + (size_t)H * NUNC;
             if constexpr (NWAVES > 1) {   // Dq: live only inside an IPM iteration's residual phase
                 L.Dq = s;
                 const size_t acl = CF == 2 ? (size_t)HB * NX * GH : (size_t)HB * NX * PS;
@@ -409,8 +411,7 @@ struct SqpKernel {
             }
         } else {
             L.P = s;   s += p_region(H, CF);
-            L.cd = s;  s += (size_t)H * NUNC;
-            L.Sig = s; s += tight_scratch(H) - (size_t)H * NUNC;
+            L.cd = s;  s += tight_scratch(H);
             if constexpr (NWAVES > 1) {
                 L.Dq = s;  s += (size_t)(H + 1) * NB;
                 L.xs = s;

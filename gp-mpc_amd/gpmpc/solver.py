@@ -71,13 +71,8 @@ class BatchSolver:
         h = ctypes.c_void_p()
         _lib.check(self.lib.gpmpc_create(spec.model_id, self.H, self.batch, self.dev_index, ctypes.byref(h)))
         self._h = h
-        self.prior = dict(spec.prior if prior_params is None else {**spec.prior, **prior_params})
-        params = _c(spec.param_vector(self.prior))
-        self._keep = [params]
-        _lib.check(self.lib.gpmpc_set_model(
-            self._h, params.ctypes.data, params.size, spec.dt, _c(spec.x_lo).ctypes.data, _c(spec.x_hi).ctypes.data,
-            _c(spec.u_lo).ctypes.data, _c(spec.u_hi).ctypes.data, _c(spec.q_diag).ctypes.data,
-            _c(spec.r_diag).ctypes.data, _c(spec.u_eq).ctypes.data, float(uh), int(cost_scaling)))
+        self._uh, self._cost_scaling = float(uh), int(cost_scaling)
+        self.set_prior(prior_params)
         self.set_options(max_iter=max_iter, tol=tol, qp_max_iter=qp_max_iter, qp_tol=qp_tol, qp_mu0=qp_mu0)
         self.set_reference(spec.reference_trajectory() if traj is None else traj)
         self.set_var_inputs(spec.var_inputs)
@@ -98,6 +93,17 @@ class BatchSolver:
             self._h = None
 
     # ------------------------------------------------------------------ configuration
+    def set_prior(self, prior_params: dict | None = None):
+        """Prior model parameters (``spec.prior`` updated by ``prior_params``), bounds, weights."""
+        spec = self.spec
+        self.prior = dict(spec.prior if prior_params is None else {**spec.prior, **prior_params})
+        params = _c(spec.param_vector(self.prior))
+        self._keep = [params]
+        _lib.check(self.lib.gpmpc_set_model(
+            self._h, params.ctypes.data, params.size, spec.dt, _c(spec.x_lo).ctypes.data, _c(spec.x_hi).ctypes.data,
+            _c(spec.u_lo).ctypes.data, _c(spec.u_hi).ctypes.data, _c(spec.q_diag).ctypes.data,
+            _c(spec.r_diag).ctypes.data, _c(spec.u_eq).ctypes.data, self._uh, self._cost_scaling))
+
     def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=50, qp_tol=1e-8, qp_mu0=1.0):
         _lib.check(self.lib.gpmpc_set_options(self._h, int(max_iter), tol, tol, tol, tol, int(qp_max_iter), qp_tol, qp_mu0))
 

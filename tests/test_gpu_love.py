@@ -106,3 +106,36 @@ def test_config5_full_size_love_matches_cpp_restatement():
             assert tg[:, 1:, :].max() > 0.0
         for b in range(B):
             x0[b] = plant.rk4(x0[b], u0[b])[0]
+
+
+@pytest.mark.parametrize("rank", [6, 40, 64, 100])
+def test_love_kernel_tile_shapes(rank):
+    """gp_love_kernel splits each root into full 16-column tiles and at most two 4-column quads on
+    the 4-block MFMA (love_tiles): rank 6 (no full tile), 40 (two quads), 64 (tiles only), 100
+    (six tiles and one quad), each against oracle.love_var with the uploaded root."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem("quad2d", 400)
+    gpp = product_gps(data, hyp)
+    H, B = 30, 64
+    gs = BatchSolver(spec, H, B)
+    gs.set_gps(gpp, variance="love", love_rank=rank, love_force=True)
+    gs.set_tightening(True, 0.95, *lqr(spec))
+    gs.reset(reset_iterate=True)
+    x0, ph = initial_states(spec, spec.reference_trajectory(), B, seed=3)
+    obs = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    u = gs.solve(obs, ts)
+    xs, us, _ = (t.cpu().numpy() for t in gs.solution())
+    gs.plant_step(obs, u, ts, out=obs)
+    gs.solve(obs, ts)
+    var = gs.variance().cpu().numpy()
+    z = np.concatenate([xs[:, :-1, :], us], axis=2).reshape(B * H, -1)
+    for g, (X, _) in enumerate(data):
+        R = gs.love_roots[g]
+        assert R is not None and R.shape[1] <= rank
+        og = SimpleNamespace(X=X.reshape(400, -1), ell=hyp[g][0], sf2=hyp[g][1], sn2=hyp[g][2])
+        ref = O.love_var(og, R, z[:, spec.var_inputs[g]])
+        err = np.abs(var[:, :, g].reshape(-1) - ref).max()
+        assert err <= 1e-9 * og.sf2, (rank, g, R.shape, err)

@@ -154,7 +154,9 @@ def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
     """The first SQP iteration of a step reads the stored iterate's linearisation (written by the
     step that produced the iterate) instead of recomputing it.  Against a solver with the cache off
     (GPMPC_LIN_CACHE=0) every output is bit-identical over a closed loop that also re-uploads the
-    GPs, resets the iterate and sets it from outside (each of which must invalidate the cache)."""
+    GPs without a reset, switches the GPs off and on, changes the prior model's parameters, re-uploads
+    with a reset, sets the iterate from outside and resets the multipliers (each of which must
+    invalidate the cache or leave it valid)."""
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
@@ -178,7 +180,19 @@ def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
     x0, ph = initial_states(spec, traj, B)
     x = torch.tensor(x0, device="cuda")
     ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
-    for k in range(9):
+    for k in range(12):
+        if k == 1:
+            for s in (on, off):   # new GPs, iterate kept (the cached rows used the old GPs)
+                s.set_gps(product_gps(data2, hyp2))
+        if k == 2:
+            for s in (on, off):   # prior-only model (gpmpc_use_gp(0))
+                s.set_gps(None)
+        if k == 8:
+            for s in (on, off):   # GPs back on
+                s.set_gps(product_gps(data, hyp))
+        if k == 10:
+            for s in (on, off):   # prior model parameters changed (gpmpc_set_model)
+                s.set_prior({key: 1.05 * v for key, v in spec.prior.items()})
         if k == 3:
             for s in (on, off):   # new GPs (GPMPC.reset after train_gp)
                 s.set_gps(product_gps(data2, hyp2))
