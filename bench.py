@@ -64,6 +64,14 @@ def gp_flops(spec, n_train, H, love_ranks=None):
     return per_lin, exps_lin, var
 
 
+def love_tiles(rank):
+    """gp_love_kernel's split of a rank-r root (gp_kernels.hip love_tiles): full 16-column tiles and
+    at most two 4-column quads."""
+    nf, rem = rank // 16, rank % 16
+    nq = (rem + 3) // 4
+    return (nf + 1, 0) if nq > 2 else (nf, nq)
+
+
 def survey_flops_per_lin(spec, n_train, H):
     """SURVEY.md §8(d)'s per-linearisation count as written there: every GP at the 4 RK4 points
     (the reference's CasADi graph evaluates u-only GPs at each of them too)."""
@@ -398,8 +406,8 @@ def run_gpu(args, rank, local_rank, world):
                                            "per step, every GP at the 4 RK4 points, as the reference computes "
                                            "them; informational, not the frac above"},
             "roofline_variance": None if var_tf is None else {
-                "kernel": ((f"gp_love_kernel<{max((r + 15) // 16 for r in solver.love_ranks if r)},true> "
-                            f"(LOVE root rank {max(r for r in solver.love_ranks if r)})")
+                "kernel": ((f"gp_love_kernel<{max([1] + [love_tiles(r)[0] for r in solver.love_ranks if r])},true> "
+                            f"(LOVE root ranks {'/'.join(str(r) for r in solver.love_ranks if r)})")
                            if any(getattr(solver, "love_ranks", None) or [])
                            else (f"gp_var_tri_kernel<{(N + 15) // 16},true>" if (N + 15) // 16 <= 16
                                  else "gp_post_kernel<true>")),
