@@ -68,6 +68,8 @@ struct gpmpc_handle {
     double* lin = nullptr;          // linearisation cache of the stored iterate (StateDev::lin)
     int32_t* lin_tag = nullptr;
     bool lin_cache = true;
+    int32_t* order = nullptr;       // cost-ordered dispatch (StateDev::order / cost)
+    uint32_t* cost = nullptr;
     double* traj = nullptr;
     double* plant_params = nullptr;
     double* tgain = nullptr;        // [H][nb][n_unc] tightening gain table (ProblemDev::tgain)
@@ -128,6 +130,8 @@ static void free_handle(gpmpc_handle* h) {
         if (p) (void)hipFree(p);
     if (h->has_prev) (void)hipFree(h->has_prev);
     if (h->lin_tag) (void)hipFree(h->lin_tag);
+    if (h->order) (void)hipFree(h->order);
+    if (h->cost) (void)hipFree(h->cost);
     if (h->scratch_i) (void)hipFree(h->scratch_i);
     if (h->scratch_d) (void)hipFree(h->scratch_d);
     for (int g = 0; g < kMaxGP; ++g) {
@@ -178,6 +182,8 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
         {(void**)&h->has_prev, B * sizeof(int32_t)},
         {(void**)&h->lin, B * H * md.nx * (h->nb + 1) * sizeof(double)},
         {(void**)&h->lin_tag, B * sizeof(int32_t)},
+        {(void**)&h->order, B * sizeof(int32_t)},
+        {(void**)&h->cost, B * sizeof(uint32_t)},
         {(void**)&h->plant_params, kMaxParams * sizeof(double)},
         {(void**)&h->scratch_i, 2 * B * sizeof(int32_t)},
         {(void**)&h->scratch_d, 4 * B * sizeof(double)},
@@ -213,6 +219,8 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
         P.condense = (ec && ec[0] == '1') ? 1 : 0;
         const char* ew = std::getenv("GPMPC_WAVES");       // "1" / "4": waves per instance (A/B)
         P.waves = ew ? std::atoi(ew) : 0;
+        const char* eo = std::getenv("GPMPC_ORDER");       // "0": dispatch in instance order (A/B)
+        P.order_dispatch = (eo && eo[0] == '0') ? 0 : 1;
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
         P.n_cu = ncu;
@@ -577,7 +585,8 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         }
     }
     // 2. the SQP step
-    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag};
+    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag,
+               h->order, h->cost};
     StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing, h->stats};
     // optional outputs go to handle-owned scratch when NULL
     if (!io.sqp_iter) io.sqp_iter = h->scratch_i;

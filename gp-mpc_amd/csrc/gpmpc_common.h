@@ -83,6 +83,9 @@ struct ProblemDev {
     int32_t waves;
     int32_t condense;
     int32_t n_cu;             // compute units of the device (set by gpmpc_create)
+    // cost-ordered dispatch (StateDev::order): on when a launch has more instances than the
+    // device holds at once (GPMPC_ORDER=0 turns it off, for A/B)
+    int32_t order_dispatch;
     GPDev gp[kMaxGP];
 };
 
@@ -102,6 +105,14 @@ struct StateDev {
     // ProblemDev::lin_gen.  Optional (NULL: always recompute).
     double* lin;
     int32_t* lin_tag;    // [B]
+    // Cost-ordered dispatch.  cost[b]: shader cycles / 16 of instance b's last solve (written by
+    // every SQP launch, optional).  order[blockIdx.x] = instance: when a launch needs more than one
+    // round of workgroups (config 5: 512 instances, one per CU), launch_sqp fills order[] with the
+    // instances by decreasing previous cost, so the dispatcher starts the slowest instances first
+    // and the fast ones fill in behind them (longest-processing-time-first; an instance's cost
+    // barely changes from one control step to the next).  NULL: identity.
+    const int32_t* order;
+    uint32_t* cost;      // [B]
 };
 
 struct StepIO {

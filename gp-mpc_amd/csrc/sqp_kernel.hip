@@ -21,6 +21,7 @@
 // obs, u_H absent), its bounds and the dynamics multiplier pi_k.  The IPM state of a stage is
 // split over lanes k and k + 32 when H + 1 <= 32 (SPL).  The Riccati recursion is sequential
 // over stages and parallel over matrix entries.  DESIGN.md §2.1 has the layouts and timings.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -326,7 +327,8 @@ struct SqpKernel {
                                      // the corrector's block gradients), corrector scratch t_j
         double *lam, *pim;           // the instance's multipliers during the step (acados memory):
                                      // bounds [H+1][2 NB], dynamics [H][NX]
-        int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
+        int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit;
+                     // ctrl + 4: the instance's start time (two ints, StateDev::cost)
     };
     // tightening: per-stage noise terms cd_k of the covariance convolution
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC; }
@@ -2503,9 +2505,11 @@ struct SqpKernel {
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
         const int lane = threadIdx.x & 63;
-        const int b = blockIdx.x;
+        const int b = S.order ? __builtin_amdgcn_readfirstlane(S.order[blockIdx.x]) : (int)blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve<CF>(smem, H);
+        // start time kept in LDS (not live in registers through the solve)
+        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(L.ctrl + 4) = __builtin_amdgcn_s_memtime();
         if constexpr (NWAVES > 1) {
             if (threadIdx.x >= 64) {   // GP helper wave
                 helper_loop<CF>(P, S, L, threadIdx.x >> 6, lane, b);
@@ -2907,6 +2911,11 @@ struct SqpKernel {
             for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
             S.has_prev[b] = good ? 1 : 0;
             if (lin_b != nullptr) S.lin_tag[b] = good ? P.lin_gen : 0;
+            if (S.cost != nullptr) {   // this solve's cycles, for the next launch's dispatch order
+                const unsigned long long c =
+                    (__builtin_amdgcn_s_memtime() - *reinterpret_cast<const unsigned long long*>(L.ctrl + 4)) >> 4;
+                S.cost[b] = (uint32_t)(c < 0xffffffffull ? c : 0xffffffffull);
+            }
             if (io.stats != nullptr) {
                 long long* st = io.stats + (size_t)b * kStatsSlots;
                 st[0] += it;
@@ -2953,6 +2962,28 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
     return hipGetLastError();
 }
 
+// order[r] = the instance of rank r by decreasing cost (ties by instance id: a permutation);
+// one thread per instance counts the instances ranked before it.  Used only for multi-round
+// launches (a few hundred to a few thousand instances: O(B^2 / threads) broadcast LDS reads).
+__global__ __launch_bounds__(256) void order_by_cost_kernel(const uint32_t* __restrict__ cost, int B,
+                                                            int32_t* __restrict__ order) {
+    __shared__ uint32_t cs[2048];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t ci = i < B ? cost[i] : 0u;
+    int rank = 0;
+    for (int j0 = 0; j0 < B; j0 += 2048) {
+        const int n = min(2048, B - j0);
+        __syncthreads();
+        for (int j = threadIdx.x; j < n; j += 256) cs[j] = cost[j0 + j];
+        __syncthreads();
+        for (int j = 0; j < n; ++j) {
+            const uint32_t cj = cs[j];
+            rank += (cj > ci || (cj == ci && j0 + j < i)) ? 1 : 0;
+        }
+    }
+    if (i < B) order[rank] = i;
+}
+
 // One wave per SIMD: every wave of an instance owns a SIMD's register file.
 template <int ID, int NW, bool SPL, int CF>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
@@ -2967,7 +2998,18 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, CF>), dim3(batch), dim3(64 * NW), lds, stream, P, S, io);
+    // instances resident at once: one wave per SIMD (4 / NW per CU), bounded by the CU's 160 KB LDS
+    const int per_cu = std::max(1, std::min(4 / NW, (int)((160 * 1024) / lds)));
+    StateDev Sl = S;
+    if (S.order != nullptr && S.cost != nullptr && P.order_dispatch && P.n_cu > 0 && batch > P.n_cu * per_cu) {
+        hipLaunchKernelGGL(order_by_cost_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, S.cost, batch,
+                           const_cast<int32_t*>(S.order));
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    } else {
+        Sl.order = nullptr;
+    }
+    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, CF>), dim3(batch), dim3(64 * NW), lds, stream, P, Sl, io);
     return hipGetLastError();
 }
 
