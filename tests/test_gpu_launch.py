@@ -72,3 +72,37 @@ def test_launch_option_validation():
     with pytest.raises(_lib.GPMPCError):
         gs.set_launch(waves=2)
     gs.set_launch(waves=0, condense=True)
+
+
+def test_cost_ordered_dispatch_is_bit_exact(monkeypatch):
+    """A launch with more instances than the device holds at once (quad3d: one instance per CU)
+    dispatches them by decreasing previous-solve cost (StateDev::order); which CU runs an instance
+    when must not change any output bit: same closed loop with GPMPC_ORDER=0 (instance order)."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    spec, data, hyp = problem("quad3d", 60)
+    spec.var_inputs = spec.gp_inputs
+    H, B, steps = 15, n_cu + 37, 3            # two rounds of workgroups
+    mats = lqr(spec)
+    gpp = product_gps(data, hyp)
+    outs = []
+    for order in ("1", "0"):
+        monkeypatch.setenv("GPMPC_ORDER", order)   # read by gpmpc_create
+        gs = BatchSolver(spec, H, B)
+        gs.set_gps(gpp)
+        gs.set_tightening(True, 0.95, *mats)
+        gs.reset(reset_iterate=True)
+        x0, ph = initial_states(spec, spec.reference_trajectory(), B, seed=5)
+        obs = torch.tensor(x0, device="cuda")
+        ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+        rec = []
+        for _ in range(steps):
+            u = gs.solve(obs, ts)
+            rec += [u.clone(), gs.status.clone(), gs.sqp_iter.clone()] + [t.clone() for t in gs.solution()]
+            gs.plant_step(obs, u, ts, out=obs)
+        outs.append([t.cpu() for t in rec])
+        assert (outs[-1][1] == 0).float().mean() > 0.9
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
