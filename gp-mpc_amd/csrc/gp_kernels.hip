@@ -292,8 +292,9 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
 // var(z) = sf2 - ||R^T k(z, X)||^2 (+ sn2) with the dense LOVE root R [npad][rank, padded to 16]
 // (gpytorch fast_pred_var, rank <= 100 for configs 4/5).  No LDS and no barriers: one wavefront =
 // 16 points, K-steps of four training rows (lane (kq, lc): point lc, row 4s + kq), four K-steps per
-// round with their exps interleaved (exp_rbf_n) and the next round's training rows and root entries
-// loaded a round ahead (the blocks of one GP run together, so its root, 3.6 MB at N = 4000 and 112
+// round, the next K-step's exp computed behind the current K-step's MFMAs, and the next round's
+// training rows and root entries loaded a round ahead (the blocks of one GP run together, so its
+// root, 3.6 MB at N = 4000 and 112
 // columns, streams through L2 once per wave generation).  Per GP (love_tiles) the root's columns
 // go to nf full 16-column tiles on v_mfma_f64_16x16x4_f64 (accumulators acc[t]) and, when at most
 // 8 columns remain, nq <= 2 four-column quads on v_mfma_f64_4x4x4_4b_f64, whose A operand is the
@@ -302,7 +303,7 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
 // point 4b + m against column n, a quarter of a 16-column tile's matrix-core cycles for the last
 // 4 of a rank-100 root's columns (the tile would be 12/16 padding).  Each GP of the launch does
 // only its own tiles (the 12-column thrust root of config 4 one tile, not the pitch root's 7).
-// The two round buffers take the kernel to ~256 VGPRs, one wave per SIMD (two measured slower).
+// The two round buffers take the kernel past 256 VGPRs, one wave per SIMD (two measured slower).
 // sf2 is applied to the squared norm (sf2^2), not to every kernel value.
 constexpr int kLoveWaves = 4;
 constexpr int kLoveMaxTiles = 8;
@@ -312,14 +313,16 @@ __host__ __device__ inline void love_tiles(int rank, int& nf, int& nq) {
     nq = (rem + 3) >> 2;
     if (nq > 2) { nf += 1; nq = 0; }
 }
-template <int NTC, bool FROM_STATE>
-__global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) {
-    const GPDev& g = pb.g[blockIdx.y];
-    const PostArgs& a = pb.a[blockIdx.y];
-    const int npad = pb.npad[blockIdx.y];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int p0 = (blockIdx.x * kLoveWaves + wave) * 16;
-    if (p0 >= a.P) return;   // wave-uniform
+// One wave's 16 points against one GP's root with NF full tiles and NQ quads, both compile-time
+// (love_dispatch picks the instantiation per block): with runtime tile counts every MFMA and every
+// root load of the K loop sat behind its own scalar branch, and the loop body was ~40 basic blocks
+// the scheduler could not work across.  Round 3: config 4 LOVE 0.339 -> 0.227 ms, config 5
+// 1.50 -> 1.06 ms (profiles/r3/ab_love_pipe/).  Each K-step's MFMAs are followed by the next
+// K-step's kernel value (one exp per lane), which runs while the matrix core works; pinning an
+// MFMA / 4-VALU interleave with sched_group_barrier measured slower (0.257 ms).
+template <int NF, int NQ, bool FROM_STATE>
+__device__ __forceinline__ void love_points(const GPDev& g, const PostArgs& a, int npad, int p0, int lane) {
+    constexpr int NFa = NF > 0 ? NF : 1, NQa = NQ > 0 ? NQ : 1;
     const int lc = lane & 15, kq = lane >> 4;
     const int p = p0 + lc;
     double z[3];
@@ -327,12 +330,10 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
     const double c = -0.5 * g.inv_ell2;
     const double4* rows = reinterpret_cast<const double4*>(g.vrows);
     const int NC = g.vroot_cols;   // row stride of the padded root
-    int nf, nq;                    // this GP's full tiles (<= NTC) and four-column quads (<= 2)
-    love_tiles(g.vroot_rank, nf, nq);
     const double* Rl = g.vroot + kq * NC + lc;                        // R[16 s4 + 4 ks + kq][16 t + lc]
-    const double* Rq = g.vroot + kq * NC + 16 * nf + (lc & 3);        // R[..][16 nf + 4 q + n]
+    const double* Rq = g.vroot + kq * NC + 16 * NF + (lc & 3);        // R[..][16 NF + 4 q + n]
     const int nv = g.nv, nround = npad / 16;
-    struct Round { double4 x[4]; double b[4][NTC]; double bq[4][2]; };
+    struct Round { double4 x[4]; double b[4][NFa]; double bq[4][NQa]; };
     auto load = [&](int s4, Round& rd) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -340,55 +341,58 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
             rd.x[ks] = rows[i < nv ? i : 0];
             const size_t ro = (size_t)(16 * s4 + 4 * ks) * NC;
 #pragma unroll
-            for (int t = 0; t < NTC; ++t) rd.b[ks][t] = (t < nf) ? Rl[ro + 16 * t] : 0.0;
+            for (int t = 0; t < NF; ++t) rd.b[ks][t] = Rl[ro + 16 * t];
 #pragma unroll
-            for (int q = 0; q < 2; ++q) rd.bq[ks][q] = (q < nq) ? Rq[ro + 4 * q] : 0.0;
+            for (int q = 0; q < NQ; ++q) rd.bq[ks][q] = Rq[ro + 4 * q];
         }
     };
-    f64x4 acc[NTC];
+    // kernel value of K-step ks of round s4 (row 16 s4 + 4 ks + kq, point lc); rows past the
+    // training set, and the round after the last (its rows stale), give 0
+    auto kval = [&](const Round& rd, int s4, int ks) {
+        const double4 r = rd.x[ks];
+        const double d0 = r.x - z[0], d1 = r.y - z[1], d2 = r.z - z[2];
+        const double e = exp_rbf(c * fma(d0, d0, fma(d1, d1, d2 * d2)));   // unused dims are zero on both sides
+        return (16 * s4 + 4 * ks + kq < nv) ? e : 0.0;
+    };
+    f64x4 acc[NFa];
 #pragma unroll
-    for (int t = 0; t < NTC; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
-    double accq[2] = {0.0, 0.0};
-    auto round = [&](int s4, const Round& rd) {
-        double kv[4];
+    for (int t = 0; t < NFa; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double accq[NQa];
+#pragma unroll
+    for (int q = 0; q < NQa; ++q) accq[q] = 0.0;
+    // the round's four K-steps; kv holds the current K-step's kernel value and leaves with the
+    // next round's first one (rows of `nx`, loaded one round ahead)
+    auto round = [&](const Round& rd, int s4, double& kv, const Round& nx) {
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-            const double4 r = rd.x[ks];
-            const double d0 = r.x - z[0], d1 = r.y - z[1], d2 = r.z - z[2];
-            kv[ks] = c * fma(d0, d0, fma(d1, d1, d2 * d2));   // unused input dims are zero on both sides
-        }
-        exp_rbf_n<4>(kv);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const double kvm = (16 * s4 + 4 * ks + kq < nv) ? kv[ks] : 0.0;
+            for (int t = 0; t < NF; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv, rd.b[ks][t], acc[t], 0, 0, 0);
 #pragma unroll
-            for (int t = 0; t < NTC; ++t)
-                if (t < nf) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kvm, rd.b[ks][t], acc[t], 0, 0, 0);
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                if (q < nq) accq[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(kvm, rd.bq[ks][q], accq[q], 0, 0, 0);
+            for (int q = 0; q < NQ; ++q) accq[q] = __builtin_amdgcn_mfma_f64_4x4x4f64(kv, rd.bq[ks][q], accq[q], 0, 0, 0);
+            kv = (ks < 3) ? kval(rd, s4, ks + 1) : kval(nx, s4 + 1, 0);
         }
     };
-    // (measured on configs 4/5: this plain form beats unconditional clamped prefetches, with or
-    // without scheduling barriers around them)
     Round r0, r1;
     load(0, r0);
+    double kv = kval(r0, 0, 0);
     int s4 = 0;
     for (; s4 + 1 < nround; s4 += 2) {
         load(s4 + 1, r1);
-        round(s4, r0);
+        round(r0, s4, kv, r1);
         if (s4 + 2 < nround) load(s4 + 2, r0);
-        round(s4 + 1, r1);
+        round(r1, s4 + 1, kv, r0);
     }
-    if (s4 < nround) round(s4, r0);
+    if (s4 < nround) round(r0, s4, kv, r1);
     // acc[t][r]: point kq + 4r, column 16 t + lc; accq[q] (lane 16 m + 4 b + n): point 4 b + m,
-    // column 16 nf + 4 q + n, i.e. row kq's point kq + 4r sits in the lanes of quad r
-    const double tq = fma(accq[0], accq[0], accq[1] * accq[1]);
+    // column 16 NF + 4 q + n, i.e. row kq's point kq + 4r sits in the lanes of quad r
+    double tq = 0.0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) tq = fma(accq[q], accq[q], tq);
     double sq[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) sq[r] = ((lc >> 2) == r) ? tq : 0.0;
 #pragma unroll
-    for (int t = 0; t < NTC; ++t)
+    for (int t = 0; t < NF; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sq[r] = fma(acc[t][r], acc[t][r], sq[r]);
 #pragma unroll
@@ -403,18 +407,37 @@ __global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) 
     }
 }
 
-template <bool FROM_STATE, int NTC = 1>
-hipError_t launch_love(const PostBatch& pb, int ntc, hipStream_t stream) {
-    if constexpr (NTC <= kLoveMaxTiles) {
-        if (ntc == NTC) {
-            int blocks = 0;
-            for (int q = 0; q < pb.n; ++q) blocks = max(blocks, (pb.a[q].P + 16 * kLoveWaves - 1) / (16 * kLoveWaves));
-            hipLaunchKernelGGL((gp_love_kernel<NTC, FROM_STATE>), dim3(blocks, pb.n), dim3(64 * kLoveWaves), 0, stream, pb);
-            return hipGetLastError();
-        }
-        return launch_love<FROM_STATE, NTC + 1>(pb, ntc, stream);
+// (NF, NQ) of the block's GP -> its instantiation (key 3 NF + NQ, NF <= kLoveMaxTiles, NQ <= 2)
+template <int K, bool FROM_STATE>
+__device__ __forceinline__ void love_dispatch(int key, const GPDev& g, const PostArgs& a, int npad, int p0, int lane) {
+    if (key == K) {
+        love_points<K / 3, K % 3, FROM_STATE>(g, a, npad, p0, lane);
+        return;
     }
-    return hipErrorInvalidValue;
+    if constexpr (K + 1 < 3 * (kLoveMaxTiles + 1)) love_dispatch<K + 1, FROM_STATE>(key, g, a, npad, p0, lane);
+}
+
+template <bool FROM_STATE>
+__global__ __launch_bounds__(64 * kLoveWaves) void gp_love_kernel(PostBatch pb) {
+    // by-value copies: the dynamically indexed kernel-argument arrays otherwise go to scratch
+    // when referenced from the dispatched bodies
+    const GPDev g = pb.g[blockIdx.y];
+    const PostArgs a = pb.a[blockIdx.y];
+    const int npad = pb.npad[blockIdx.y];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int p0 = (blockIdx.x * kLoveWaves + wave) * 16;
+    if (p0 >= a.P) return;   // wave-uniform
+    int nf, nq;              // this GP's full tiles and four-column quads
+    love_tiles(g.vroot_rank, nf, nq);
+    love_dispatch<1, FROM_STATE>(3 * nf + nq, g, a, npad, p0, lane);
+}
+
+template <bool FROM_STATE>
+hipError_t launch_love(const PostBatch& pb, hipStream_t stream) {
+    int blocks = 0;
+    for (int q = 0; q < pb.n; ++q) blocks = max(blocks, (pb.a[q].P + 16 * kLoveWaves - 1) / (16 * kLoveWaves));
+    hipLaunchKernelGGL((gp_love_kernel<FROM_STATE>), dim3(blocks, pb.n), dim3(64 * kLoveWaves), 0, stream, pb);
+    return hipGetLastError();
 }
 
 template <bool FROM_STATE, int NT = 1>
@@ -450,17 +473,13 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
     }
     if (blocks == 0 || pb.n == 0) return hipSuccess;
     bool love = true;   // every entry variance-only with a LOVE root of <= 128 columns
-    int tmax = 1;       // the launch's widest full-tile count (love_tiles)
     for (int q = 0; q < pb.n; ++q) {
         love = love && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].vroot != nullptr &&
                pb.g[q].vroot_cols % 16 == 0 && pb.g[q].vroot_cols <= 16 * kLoveMaxTiles &&
                pb.g[q].vroot_rank >= 1 && pb.g[q].vroot_rank <= pb.g[q].vroot_cols;
-        int nf = 0, nq = 0;
-        love_tiles(pb.g[q].vroot_rank, nf, nq);
-        tmax = max(tmax, nf);
     }
     if (love)
-        return from_state ? launch_love<true>(pb, tmax, stream) : launch_love<false>(pb, tmax, stream);
+        return from_state ? launch_love<true>(pb, stream) : launch_love<false>(pb, stream);
     bool tri = true;   // every entry variance-only with the same npad <= 256
     for (int q = 0; q < pb.n; ++q)
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&
