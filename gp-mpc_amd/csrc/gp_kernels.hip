@@ -65,7 +65,11 @@ __device__ __forceinline__ double dpp_row_sum(double v) {
 __host__ __device__ inline int post_ct(int npad) { return npad / 16 < kMaxCT ? npad / 16 : kMaxCT; }
 __host__ __device__ inline int post_stride(int ct) { return 16 * (ct | 1); }
 
-template <bool FROM_STATE>
+// FULL: every column group of the launch has kMaxCT tiles (npad >= 256 for L^-T, >= 256 root
+// columns): each panel is staged whole, with zeros for the skipped triangle and past the last
+// column, so the K loop runs every tile unconditionally (no scalar branch per MFMA; the few zero
+// tiles of each group's diagonal block cost less than the branches did).
+template <bool FROM_STATE, bool FULL>
 __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) {
     extern __shared__ __attribute__((aligned(16))) double panel[];
     const GPDev& g = pb.g[blockIdx.y];
@@ -122,24 +126,44 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
             // staged copy of panel `pan` (columns of tiles >= max(pan, t0) of this group)
             double2 stage[4];
             auto fetch = [&](int pan) {
-                const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
+                if constexpr (FULL) {
+                    // the whole 16 x 256 panel: zeros below the diagonal (tiles < pan) and past ncols
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = 2 * (tid + j * 64 * kPostWaves);
-                    const int row = e / w, col = e - row * w;
-                    stage[j] = (row < 16)
-                                   ? *reinterpret_cast<const double2*>(Bm + (size_t)(16 * pan + row) * ncols +
-                                                                       16 * (t0 + lt0) + col)
-                                   : double2{0.0, 0.0};
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 2 * (tid + j * 64 * kPostWaves);
+                        const int row = e >> 8, col = e & 255, gc = 16 * t0 + col;
+                        const bool nz = gc < ncols && !(tri && gc < 16 * pan);
+                        stage[j] = nz ? *reinterpret_cast<const double2*>(Bm + (size_t)(16 * pan + row) * ncols + gc)
+                                      : double2{0.0, 0.0};
+                    }
+                } else {
+                    const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 2 * (tid + j * 64 * kPostWaves);
+                        const int row = e / w, col = e - row * w;
+                        stage[j] = (row < 16)
+                                       ? *reinterpret_cast<const double2*>(Bm + (size_t)(16 * pan + row) * ncols +
+                                                                           16 * (t0 + lt0) + col)
+                                       : double2{0.0, 0.0};
+                    }
                 }
             };
             auto deposit = [&](int pan, double* buf) {
-                const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
+                if constexpr (FULL) {
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int e = 2 * (tid + j * 64 * kPostWaves);
-                    const int row = e / w, col = e - row * w;
-                    if (row < 16) *reinterpret_cast<double2*>(buf + row * Wp + 16 * lt0 + col) = stage[j];
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 2 * (tid + j * 64 * kPostWaves);
+                        *reinterpret_cast<double2*>(buf + (e >> 8) * Wp + (e & 255)) = stage[j];
+                    }
+                } else {
+                    const int lt0 = tri ? max(pan - t0, 0) : 0, w = 16 * (tn - lt0);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int e = 2 * (tid + j * 64 * kPostWaves);
+                        const int row = e / w, col = e - row * w;
+                        if (row < 16) *reinterpret_cast<double2*>(buf + row * Wp + 16 * lt0 + col) = stage[j];
+                    }
                 }
             };
             f64x4 acc[kMaxCT];
@@ -161,7 +185,8 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
                     const double* brow = buf + (4 * ks + kq) * Wp + lc;
 #pragma unroll
                     for (int t = 0; t < kMaxCT; ++t)
-                        if (t >= lt0 && t < tn) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv, brow[16 * t], acc[t], 0, 0, 0);
+                        if (FULL || (t >= lt0 && t < tn))
+                            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv, brow[16 * t], acc[t], 0, 0, 0);
                 }
                 if (pan + 1 < npan) deposit(pan + 1, panel + ((pan + 1) & 1) * 16 * Wp);
                 __syncthreads();
@@ -491,16 +516,22 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
     static bool attr = false;
     if (!attr) {
         const int mx = 2 * 16 * post_stride(kMaxCT) * (int)sizeof(double);
-        hipError_t e = hipFuncSetAttribute((const void*)gp_post_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)gp_post_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
-        if (e != hipSuccess) return e;
+        for (const void* k : {(const void*)gp_post_kernel<true, false>, (const void*)gp_post_kernel<false, false>,
+                              (const void*)gp_post_kernel<true, true>, (const void*)gp_post_kernel<false, true>}) {
+            const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+            if (e != hipSuccess) return e;
+        }
         attr = true;
     }
-    if (from_state)
-        hipLaunchKernelGGL(gp_post_kernel<true>, dim3(blocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
-    else
-        hipLaunchKernelGGL(gp_post_kernel<false>, dim3(blocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
+    bool full = true;   // every variance entry's column groups have kMaxCT tiles
+    for (int q = 0; q < pb.n; ++q) {
+        const bool var = pb.a[q].var != nullptr && (pb.g[q].linvT != nullptr || pb.g[q].vroot != nullptr);
+        const int ncols = pb.g[q].vroot ? pb.g[q].vroot_cols : pb.npad[q];
+        full = full && (!var || post_ct(ncols) == kMaxCT);
+    }
+    auto* k = from_state ? (full ? gp_post_kernel<true, true> : gp_post_kernel<true, false>)
+                         : (full ? gp_post_kernel<false, true> : gp_post_kernel<false, false>);
+    hipLaunchKernelGGL(k, dim3(blocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
     return hipGetLastError();
 }
 
