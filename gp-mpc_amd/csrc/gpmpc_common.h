@@ -105,8 +105,9 @@ struct StateDev {
     // ProblemDev::lin_gen.  Optional (NULL: always recompute).
     double* lin;
     int32_t* lin_tag;    // [B]
-    // Cost-ordered dispatch.  cost[b]: shader cycles / 16 of instance b's last solve (written by
-    // every SQP launch, optional).  order[blockIdx.x] = instance: when a launch needs more than one
+    // Cost-ordered dispatch.  cost[b]: the work of instance b's last solve, SQP iterations and IPM
+    // iterations weighted by their measured cycle ratio (written by every SQP launch, optional;
+    // in-kernel timestamps cost the single-wave kernel 48 B/lane of scratch).  order[blockIdx.x] = instance: when a launch needs more than one
     // round of workgroups (config 5: 512 instances, one per CU), launch_sqp fills order[] with the
     // instances by decreasing previous cost, so the dispatcher starts the slowest instances first
     // and the fast ones fill in behind them (longest-processing-time-first; an instance's cost

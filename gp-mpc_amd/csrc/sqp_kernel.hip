@@ -289,6 +289,10 @@ struct SqpKernel {
     using M = Model<ID>;
     static constexpr int NX = M::NX, NU = M::NU, NB = M::NB, NGP = M::NGP, NUNC = M::NUNC;
     static constexpr int GS = NB + 1;   // row stride of G'_k = [A_k | B_k | c_k]
+    // cost of a solve for the dispatch order (StateDev::cost) in half IPM iterations: an SQP
+    // iteration's linearisation costs ~1.4 IPM iterations on the single-tile models and ~2.6 on
+    // quad3d (FITC tile sums over M = 2000; phase tables of DESIGN §2.1 / §4)
+    static constexpr int kCostLin = (NB + 1 > 16) ? 5 : 3;
     static constexpr int PS = NX + 1;   // row stride of P'_k = [P_k | p_k] and K'_k = [K_k | kff_k]
     static constexpr int CB = 4;        // tangent column block
     static constexpr int NCB = (NB + CB - 1) / CB;
@@ -327,8 +331,7 @@ struct SqpKernel {
                                      // the corrector's block gradients), corrector scratch t_j
         double *lam, *pim;           // the instance's multipliers during the step (acados memory):
                                      // bounds [H+1][2 NB], dynamics [H][NX]
-        int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit;
-                     // ctrl + 4: the instance's start time (two ints, StateDev::cost)
+        int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
     };
     // tightening: per-stage noise terms cd_k of the covariance convolution
     __host__ __device__ static size_t tight_scratch(int H) { return (size_t)H * NUNC; }
@@ -2508,8 +2511,6 @@ struct SqpKernel {
         const int b = S.order ? __builtin_amdgcn_readfirstlane(S.order[blockIdx.x]) : (int)blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve<CF>(smem, H);
-        // start time kept in LDS (not live in registers through the solve)
-        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(L.ctrl + 4) = __builtin_amdgcn_s_memtime();
         if constexpr (NWAVES > 1) {
             if (threadIdx.x >= 64) {   // GP helper wave
                 helper_loop<CF>(P, S, L, threadIdx.x >> 6, lane, b);
@@ -2911,11 +2912,8 @@ struct SqpKernel {
             for (int q = 0; q < 4; ++q) io.res[(size_t)b * 4 + q] = res[q];
             S.has_prev[b] = good ? 1 : 0;
             if (lin_b != nullptr) S.lin_tag[b] = good ? P.lin_gen : 0;
-            if (S.cost != nullptr) {   // this solve's cycles, for the next launch's dispatch order
-                const unsigned long long c =
-                    (__builtin_amdgcn_s_memtime() - *reinterpret_cast<const unsigned long long*>(L.ctrl + 4)) >> 4;
-                S.cost[b] = (uint32_t)(c < 0xffffffffull ? c : 0xffffffffull);
-            }
+            if (S.cost != nullptr)   // this solve's work, for the next launch's dispatch order
+                S.cost[b] = (uint32_t)(kCostLin * it + 2 * qp_total);
             if (io.stats != nullptr) {
                 long long* st = io.stats + (size_t)b * kStatsSlots;
                 st[0] += it;
