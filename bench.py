@@ -406,11 +406,11 @@ def run_gpu(args, rank, local_rank, world):
                                            "per step, every GP at the 4 RK4 points, as the reference computes "
                                            "them; informational, not the frac above"},
             "roofline_variance": None if var_tf is None else {
-                "kernel": ((f"gp_love_kernel<{max([1] + [love_tiles(r)[0] for r in solver.love_ranks if r])},true> "
-                            f"(LOVE root ranks {'/'.join(str(r) for r in solver.love_ranks if r)})")
+                "kernel": ((f"gp_love_kernel<true> (LOVE root ranks {'/'.join(str(r) for r in solver.love_ranks if r)}, "
+                            f"full tiles/quads {'/'.join('%d+%d' % love_tiles(r) for r in solver.love_ranks if r)})")
                            if any(getattr(solver, "love_ranks", None) or [])
                            else (f"gp_var_tri_kernel<{(N + 15) // 16},true>" if (N + 15) // 16 <= 16
-                                 else "gp_post_kernel<true>")),
+                                 else "gp_post_kernel<true,FULL>")),
                 "bound": "mfma", "achieved": var_tf, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": var_tf / FP64_PEAK_TFLOPS, "ms_per_launch": var_ms},
             "exp_ceiling": {"exps_per_launch": exps_launch, "achieved_per_s": exps_launch / (sqp_ms * 1e-3),
