@@ -2999,7 +2999,10 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
     // instances resident at once: one wave per SIMD (4 / NW per CU), bounded by the CU's 160 KB LDS
     const int per_cu = std::max(1, std::min(4 / NW, (int)((160 * 1024) / lds)));
     StateDev Sl = S;
-    if (S.order != nullptr && S.cost != nullptr && P.order_dispatch && P.n_cu > 0 && batch > P.n_cu * per_cu) {
+    // (rank by counting: O(B^2) comparisons, a few microseconds up to ~16 k instances; larger
+    // launches keep instance order rather than pay for it)
+    if (S.order != nullptr && S.cost != nullptr && P.order_dispatch && P.n_cu > 0 && batch > P.n_cu * per_cu &&
+        batch <= 16384) {
         hipLaunchKernelGGL(order_by_cost_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, S.cost, batch,
                            const_cast<int32_t*>(S.order));
         const hipError_t e = hipGetLastError();
