@@ -632,7 +632,7 @@ gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev,
 
 gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves, int32_t condense) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
-    if (waves != 0 && waves != 1 && waves != 4) return fail(GPMPC_ERR_ARG, "waves must be 0 (auto), 1 or 4");
+    if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(GPMPC_ERR_ARG, "waves must be 0 (auto), 1, 2 or 4");
     h->P.waves = waves;
     h->P.condense = condense ? 1 : 0;
     return GPMPC_OK;

@@ -280,7 +280,7 @@ __device__ __attribute__((noinline)) void gp_tiles_dispatch(const double* tX, co
 }
 
 // Waves per instance: the wide model (quad3d) always runs four (its LDS allows one instance per CU);
-// the single-tile models run one, or four when the batch leaves SIMDs idle (launch_sqp_step).
+// the single-tile models run one, or two / four when the batch leaves SIMDs idle (launch_sqp_step).
 template <int ID>
 constexpr int kDefaultWaves = (Model<ID>::NB + 1 > 16) ? 4 : 1;
 
@@ -319,7 +319,7 @@ struct SqpKernel {
     // main wave runs the recursions.  The single-tile models use the same protocol when the batch
     // is small enough for every instance to have a CU (B <= CUs): the idle SIMDs then do that work.
     static constexpr int NWAVES = NW;
-    static_assert(NW == 1 || NW == 4, "one wave per instance or four (one per SIMD of the CU)");
+    static_assert(NW == 1 || NW == 4 || (NW == 2 && kMfma), "one wave per instance, two (single-tile models) or four: one per SIMD");
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
 
@@ -3023,15 +3023,18 @@ hipError_t launch_sqp_cf(const ProblemDev& P, const StateDev& S, const StepIO& i
     return launch_sqp_variant<ID, NW, SPL, 1>(P, S, io, batch, stream);
 }
 
-// waves per instance for this launch: the model's default, or (single-tile models) four when every
-// instance can have a CU of its own (batch <= CUs) and the request allows it (P.waves: 0 = auto)
+// waves per instance for this launch: the model's default, or (single-tile models) as many as the
+// batch leaves SIMDs for -- four when every instance can have a CU of its own (batch <= CUs), two
+// when two instances share a CU (batch <= 2 CUs), else one -- unless the request fixes it (P.waves:
+// 0 = auto)
 template <int ID>
 int sqp_waves(const ProblemDev& P, int batch) {
     if constexpr (kDefaultWaves<ID> > 1) {
         return kDefaultWaves<ID>;
     } else {
-        if (P.waves == 1 || P.waves == 4) return P.waves;
-        return (P.n_cu > 0 && batch <= P.n_cu) ? 4 : 1;
+        if (P.waves == 1 || P.waves == 2 || P.waves == 4) return P.waves;
+        if (P.n_cu <= 0) return 1;
+        return batch <= P.n_cu ? 4 : (batch <= 2 * P.n_cu ? 2 : 1);
     }
 }
 
@@ -3040,8 +3043,11 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
     if constexpr (kDefaultWaves<ID> == 1) {
         // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
         const bool spl = P.H + 1 <= 32;
-        if (sqp_waves<ID>(P, batch) == 4)
+        const int nw = sqp_waves<ID>(P, batch);
+        if (nw == 4)
             return spl ? launch_sqp_cf<ID, 4, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 4, false>(P, S, io, batch, stream);
+        if (nw == 2)
+            return spl ? launch_sqp_cf<ID, 2, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 2, false>(P, S, io, batch, stream);
         return spl ? launch_sqp_cf<ID, 1, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 1, false>(P, S, io, batch, stream);
     } else {
         // multi-wave models split the IPM state over their waves instead (WSPL)

@@ -194,7 +194,7 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr(), self.STATS_SLOTS))
 
     def set_launch(self, waves: int = 0, condense: bool = False):
-        """SQP-kernel launch shape (gpmpc_set_launch): waves per instance (0 auto, 1, 4) and the
+        """SQP-kernel launch shape (gpmpc_set_launch): waves per instance (0 auto, 1, 2, 4) and the
         condensed stage-pair recursions.  Performance options; results agree to rounding."""
         _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves), int(bool(condense))))
 

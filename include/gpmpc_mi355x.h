@@ -171,9 +171,9 @@ gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* para
 
 /* Launch shape of the SQP kernel (no reference counterpart: the reference solves one instance).
  *   waves     0 = auto: one wavefront per instance, or -- for the models whose stage fits one MFMA
- *             tile (quad2d, cartpole) -- four per instance when batch <= the device's compute units,
- *             so the SIMDs that would idle take the GP tile sums and the IPM's elementwise work;
- *             1 / 4 force either (quad3d always runs four).
+ *             tile (quad2d, cartpole) -- four per instance when batch <= the device's compute units
+ *             and two when batch <= twice that, so the SIMDs that would idle take the GP tile sums;
+ *             1 / 2 / 4 force a count (quad3d always runs four).
  *   condense  1 = the Newton systems' Riccati recursions run over condensed stage pairs when H is
  *             even (single-tile models), 0 (default) = stage by stage.
  * Results are identical up to floating-point rounding; both are performance options. */

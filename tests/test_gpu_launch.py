@@ -23,7 +23,7 @@ def _torch():
     return torch
 
 
-@pytest.mark.parametrize("waves,condense", [(1, 0), (1, 1), (4, 0), (4, 1)])
+@pytest.mark.parametrize("waves,condense", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0), (4, 1)])
 @pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 12, 4), ("cartpole", 50, 20, 12, 4),
                                                ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
 def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, condense):
@@ -70,7 +70,7 @@ def test_launch_option_validation():
     spec, _, _ = problem("quad2d", 20)
     gs = BatchSolver(spec, 10, 2)
     with pytest.raises(_lib.GPMPCError):
-        gs.set_launch(waves=2)
+        gs.set_launch(waves=3)
     gs.set_launch(waves=0, condense=True)
 
 
