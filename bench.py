@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
 """GP-MPC control steps/sec on MI355X (BASELINE.json metric, config 3 per GPU).
 
-Workload (per GPU, weak scaling): 2D quadrotor GP-MPC, N=200 GP training points, H=30,
-B=1024 independent MPC instances.  One "step" = one batched ``select_action`` over the B
+Workload (BASELINE.json metric): 2D quadrotor GP-MPC, N=200 GP training points, H=30, a global
+batch of B=1024 independent MPC instances, split over the N GPUs in contiguous slices (strong
+scaling, the metric's "batch 1024 @1/2/4/8 GPU"; ``--batch B`` instead fixes B instances per GPU:
+weak scaling).  One "step" = one batched ``select_action`` over the B
 instances (variance kernel -> tightening + SQP-GN/IPM kernel) followed by the synthetic
 plant kernel that produces the next observation.  Inputs are resident in HBM; the GP,
 hyperparameters, initial states and reference are synthetic and seeded
 (gpmpc/synthetic.py).  N>1: one process per GPU (torch.distributed, RCCL), instances
-sharded by rank, no collective in the data path; barrier + max-over-ranks timing.
+sharded by rank, no collective in the data path; barrier + max-over-ranks timing.  With N>1 and
+the default partition the line also carries ``weak_per_gpu``: the same step with 1024 instances on
+every GPU (a second timed run, after the strong one).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -35,6 +39,7 @@ import numpy as np  # noqa: E402
 from gpmpc.launch import maybe_spawn, rank_env  # noqa: E402  (no GPU/torch.cuda use)
 
 METRIC = "GP-MPC control steps/sec, 2D quadrotor H=30 N=200, batch 1024 @1/2/4/8 GPU"
+METRIC_GLOBAL_BATCH = 1024   # the metric's batch, split over the GPUs (strong scaling)
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 dense peak (vector and matrix are equal on gfx950)
 # exp_rbf (csrc/gpmpc_common.h) is 15 f64 VALU operations + 2 integer ones: the VALU ceiling of
 # exps is the FP64 FMA-lane rate (78.6 TFLOP/s / 2) over 17 issued instructions
@@ -153,10 +158,13 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU (weak scaling)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="instances per GPU (weak scaling); default: the metric's global batch split over the GPUs")
     ap.add_argument("--global-batch", type=int, default=0,
                     help="total instances over all GPUs, contiguous B/G slices per rank (strong scaling, "
-                         "SURVEY.md 8(e)); overrides --batch")
+                         f"SURVEY.md 8(e)); the default partition when --batch is not given ({METRIC_GLOBAL_BATCH})")
+    ap.add_argument("--no-weak-secondary", action="store_true",
+                    help="N>1, default partition: skip the second, weak-scaled run (weak_per_gpu)")
     ap.add_argument("--model", default="quad2d")
     ap.add_argument("--n-train", type=int, default=200)
     ap.add_argument("--horizon", type=int, default=30)
@@ -176,6 +184,18 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal: host sleep instead of the GPU step (launcher / shards / timing)")
     return ap.parse_args(argv)
+
+
+def resolve_partition(args) -> bool:
+    """Fix the instance partition: ``--global-batch G`` or, without ``--batch``, the metric's global
+    batch (strong scaling); ``--batch B`` alone: B per GPU (weak).  Returns True when the weak
+    secondary run applies (the default partition, so the line can show both figures)."""
+    default = not args.global_batch and args.batch is None
+    if default:
+        args.global_batch = METRIC_GLOBAL_BATCH
+    if args.global_batch:
+        args.batch = None
+    return default and not args.no_weak_secondary
 
 
 def workload_name(spec, args, world=1):
@@ -213,7 +233,10 @@ def reduce_timing(dist, elapsed, extra, dev=None):
     return t.tolist()
 
 
-def run_dry(args, rank, world):
+WEAK_BATCH = 1024   # weak_per_gpu: instances per GPU of the secondary run (config 3's per-GPU batch)
+
+
+def run_dry(args, rank, world, weak_secondary=False):
     """CPU rehearsal of the multi-rank bench: the same shards, barriers and max-over-ranks
     timing around a host sleep of (1 + rank) ms per step."""
     from gpmpc import distributed as D
@@ -221,24 +244,33 @@ def run_dry(args, rank, world):
 
     dist = init_dist(world, 0, use_gpu=False)
     spec = get_spec(args.model)
+
+    def timed(ids):
+        for _ in range(args.warmup):
+            time.sleep(1e-3 * (1 + rank))
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            time.sleep(1e-3 * (1 + rank))
+        local = time.perf_counter() - t0   # this rank's own work, before the closing barrier
+        if dist is not None:
+            dist.barrier()
+        elapsed, = reduce_timing(dist, time.perf_counter() - t0, [])
+        shards = [None] * world
+        if dist is not None:
+            dist.all_gather_object(shards, [ids.start, ids.stop, local])
+        else:
+            shards = [[ids.start, ids.stop, local]]
+        return elapsed, shards
+
     ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
-    for _ in range(args.warmup):
-        time.sleep(1e-3 * (1 + rank))
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        time.sleep(1e-3 * (1 + rank))
-    local = time.perf_counter() - t0   # this rank's own work, before the closing barrier
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed, = reduce_timing(dist, elapsed, [])
-    shards = [None] * world
-    if dist is not None:
-        dist.all_gather_object(shards, [ids.start, ids.stop, local])
-    else:
-        shards = [[ids.start, ids.stop, local]]
+    elapsed, shards = timed(ids)
+    weak = None
+    if weak_secondary and world > 1:
+        w_el, w_shards = timed(D.shard_range(WEAK_BATCH, rank))
+        weak = {"value": WEAK_BATCH * world * args.steps / w_el, "batch_per_gpu": WEAK_BATCH,
+                "ms_per_step": w_el / args.steps * 1e3, "scaling": "weak", "shards": w_shards}
     if rank == 0:
         total = args.global_batch or args.batch * world
         print(json.dumps({"metric": METRIC, "value": total * args.steps / elapsed, "unit": "control steps/s",
@@ -247,15 +279,15 @@ def run_dry(args, rank, world):
                           "scaling": "strong" if args.global_batch else "weak",
                           "vs_baseline": None, "dtype": "f64", "data": "dry run (host sleep, no GPU)",
                           "config": {"workload": workload_name(spec, args, world), "model": spec.name,
-                                     "global_batch": total, "horizon": args.horizon, "n_train": args.n_train,
-                                     "parallelism": f"instances sharded over {world} rank(s)"},
-                          "shards": shards}))
+                                     "global_batch": total, "batch_per_gpu": len(ids), "horizon": args.horizon,
+                                     "n_train": args.n_train, "parallelism": f"instances sharded over {world} rank(s)"},
+                          "shards": shards, "weak_per_gpu": weak}))
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
 
 
-def run_gpu(args, rank, local_rank, world):
+def run_gpu(args, rank, local_rank, world, weak_secondary=False):
     import torch
 
     # one rank per GPU (local_rank modulo the visible GPUs only matters for a rehearsal of the
@@ -275,11 +307,6 @@ def run_gpu(args, rank, local_rank, world):
     if args.var_inputs == "dynamics":
         spec.var_inputs = spec.gp_inputs
     H, N = args.horizon, args.n_train
-    # instances of this rank: contiguous global ids (weak: rank*B .. rank*B+B-1; strong: the rank's
-    # slice of the global batch), no collective in the data path
-    ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
-    B = len(ids)
-    total_instances = args.global_batch or args.batch * world
     data = D.replicate_training_data(make_training_data(spec, N, seed=1), device=dev)  # GP replicated on every rank
     hyp = DEFAULT_HYPERS[spec.name]
     gps = []
@@ -290,8 +317,6 @@ def run_gpu(args, rank, local_rank, world):
     Q, R = np.diag(spec.q_diag), np.diag(spec.r_diag)
     dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
     lqr_mats = setup_prior_dynamics(dfdx, dfdu, Q, R, spec.dt)
-
-    solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
     fitc = None
     if args.fitc:
         from gpmpc.gpmpc import GPMPC
@@ -301,61 +326,88 @@ def run_gpu(args, rank, local_rank, world):
         me = type("Me", (), {})()
         me.gaussian_process, me.np_random = gps, np.random.default_rng(1337)
         fitc = GPMPC.precompute_sparse_posterior_mean(me, min(args.fitc, N))
-    solver.set_gps(gps, fitc=fitc, variance=args.variance)
-    solver.set_tightening(True, 0.95, *lqr_mats)
-    solver.reset(reset_iterate=True)
     traj = spec.reference_trajectory()
-    x0_all, phase_all = initial_states(spec, traj, total_instances, seed=1)
-    obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
-    tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
-    stats_buf = torch.zeros(B, BatchSolver.STATS_SLOTS, dtype=torch.int64, device=dev)   # filled by the SQP kernel
-    solver.set_stats(stats_buf)
 
-    def step():
-        u0 = solver.solve(obs, tstep)
-        solver.plant_step(obs, u0, tstep, out=obs)
+    def measure(ids, total_instances):
+        """One timed closed-loop run of this rank's instances ``ids`` (global ids of a
+        ``total_instances`` job): W untimed steps, barrier + synchronize, K timed steps, barrier +
+        synchronize, max over ranks."""
+        B = len(ids)
+        solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
+        solver.set_gps(gps, fitc=fitc, variance=args.variance)
+        solver.set_tightening(True, 0.95, *lqr_mats)
+        solver.reset(reset_iterate=True)
+        x0_all, phase_all = initial_states(spec, traj, total_instances, seed=1)
+        obs = torch.tensor(x0_all[ids.start:ids.stop], device=dev)
+        tstep = torch.tensor(phase_all[ids.start:ids.stop], dtype=torch.int32, device=dev)
+        stats_buf = torch.zeros(B, BatchSolver.STATS_SLOTS, dtype=torch.int64, device=dev)   # filled by the SQP kernel
+        solver.set_stats(stats_buf)
 
-    solver.set_profiling(True)   # warm-up runs the timed body exactly (events)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    solver.kernel_time_list()  # drop warm-up events
-    stats_buf.zero_()
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    t_enqueue = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    solver.set_profiling(False)
-    kt = solver.kernel_time_list()
-    sqp_list, var_list = kt["sqp_ms"], kt["var_ms"]
-    elapsed, sqp_sum, var_sum = reduce_timing(dist, elapsed, [sum(sqp_list), sum(var_list)], dev)
-    tot = stats_buf.sum(0).to(torch.float64)
-    mx = stats_buf.max(0).values.to(torch.float64)
-    sums, status_counts, maxes = torch.cat([tot[:2], tot[9:10]]), tot[2:7].clone(), mx[7:9].clone()
-    if dist is not None:
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
-        dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
-        dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
-    value = total_instances * args.steps / elapsed
-    sqp_mean = float(sums[0]) / (total_instances * args.steps)
-    lin_mean = float(sums[2]) / (total_instances * args.steps)   # linearisations computed per instance-step
-    qp_mean = float(sums[1]) / (total_instances * args.steps)
+        def step():
+            u0 = solver.solve(obs, tstep)
+            solver.plant_step(obs, u0, tstep, out=obs)
+
+        solver.set_profiling(True)   # warm-up runs the timed body exactly (events)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        solver.kernel_time_list()  # drop warm-up events
+        stats_buf.zero_()
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        t_enqueue = time.perf_counter() - t0
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        solver.set_profiling(False)
+        kt = solver.kernel_time_list()
+        sqp_list, var_list = kt["sqp_ms"], kt["var_ms"]
+        elapsed, sqp_sum, var_sum = reduce_timing(dist, elapsed, [sum(sqp_list), sum(var_list)], dev)
+        tot = stats_buf.sum(0).to(torch.float64)
+        mx = stats_buf.max(0).values.to(torch.float64)
+        sums, status_counts, maxes = torch.cat([tot[:2], tot[9:10]]), tot[2:7].clone(), mx[7:9].clone()
+        if dist is not None:
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+            dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
+            dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
+        n_is = total_instances * args.steps
+        return {"B": B, "solver": solver, "elapsed": elapsed, "t_enqueue": t_enqueue, "sqp_list": sqp_list,
+                "var_list": var_list, "sqp_sum": sqp_sum, "var_sum": var_sum, "x0_all": x0_all,
+                "phase_all": phase_all, "value": total_instances * args.steps / elapsed,
+                "sqp_mean": float(sums[0]) / n_is, "lin_mean": float(sums[2]) / n_is, "qp_mean": float(sums[1]) / n_is,
+                "status_counts": status_counts, "maxes": maxes}
+
+    # instances of this rank: contiguous global ids (strong: the rank's slice of the global batch;
+    # weak: rank*B .. rank*B+B-1), no collective in the data path
+    ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
+    total_instances = args.global_batch or args.batch * world
+    m = measure(ids, total_instances)
+    weak = None
+    if weak_secondary and world > 1:
+        w = measure(D.shard_range(WEAK_BATCH, rank), WEAK_BATCH * world)
+        weak = {"value": w["value"], "batch_per_gpu": WEAK_BATCH, "global_batch": WEAK_BATCH * world,
+                "ms_per_step": w["elapsed"] / args.steps * 1e3, "scaling": "weak",
+                "sqp_kernel_ms": w["sqp_sum"] / max(len(w["sqp_list"]), 1),
+                "status_counts": {str(i): int(w["status_counts"][i]) for i in range(5)},
+                "note": "secondary run: the same step with 1024 instances on every GPU (per-GPU work fixed)"}
+    B, solver, elapsed = m["B"], m["solver"], m["elapsed"]
+    sqp_list, var_list = m["sqp_list"], m["var_list"]
+    sqp_mean, lin_mean, qp_mean = m["sqp_mean"], m["lin_mean"], m["qp_mean"]
+    status_counts, maxes = m["status_counts"], m["maxes"]
 
     if rank == 0:
         per_lin, exps_lin, var_flops = gp_flops(spec, N, H, getattr(solver, "love_ranks", None))
         # dominant kernel: the SQP kernel; linearisations computed per instance-step = sqp_iter + 1,
         # minus the one read from the linearisation cache (lin_mean, counted by the kernel)
-        sqp_ms = sqp_sum / max(len(sqp_list), 1)
+        sqp_ms = m["sqp_sum"] / max(len(sqp_list), 1)
         flops_sqp = B * lin_mean * per_lin          # per launch (one rank's batch)
         achieved = flops_sqp / (sqp_ms * 1e-3) / 1e12
-        var_ms = var_sum / max(len(var_list), 1)
+        var_ms = m["var_sum"] / max(len(var_list), 1)
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if var_list else None
         exps_launch = B * lin_mean * exps_lin
         workload = workload_name(spec, args, world)
@@ -374,12 +426,12 @@ def run_gpu(args, rank, local_rank, world):
             traffic = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
-            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, x0_all, phase_all, list(ids),
+            cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, m["x0_all"], m["phase_all"], list(ids),
                                args.warmup, args.steps, fitc=fitc, love_roots=solver.love_roots)
         sq = np.array(sqp_list) if sqp_list else np.zeros(1)
         out = {
             "metric": METRIC,
-            "value": value,
+            "value": m["value"],
             "unit": "control steps/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -422,7 +474,7 @@ def run_gpu(args, rank, local_rank, world):
             "sqp_kernel_ms_per_step_distribution": {
                 "min": float(sq.min()), "p50": float(np.median(sq)), "p90": float(np.percentile(sq, 90)),
                 "max": float(sq.max()), "per_step": [round(float(v), 4) for v in sq]},
-            "host_enqueue_ms_per_step": t_enqueue / args.steps * 1e3,
+            "host_enqueue_ms_per_step": m["t_enqueue"] / args.steps * 1e3,
             "sqp_iter_mean": sqp_mean,
             "linearisations_per_step": lin_mean,
             "sqp_iter_max": int(maxes[0]),
@@ -430,6 +482,7 @@ def run_gpu(args, rank, local_rank, world):
             "qp_iter_max_per_step": int(maxes[1]),
             "status_counts": {str(i): int(status_counts[i]) for i in range(5)},
             "exps_per_sqp_launch": exps_launch,
+            "weak_per_gpu": weak,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
@@ -446,10 +499,11 @@ def main(argv=None):
     rank, local_rank, world = rank_env()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    weak_secondary = resolve_partition(args)
     if args.dry_run:
-        run_dry(args, rank, world)
+        run_dry(args, rank, world, weak_secondary)
     else:
-        run_gpu(args, rank, local_rank, world)
+        run_gpu(args, rank, local_rank, world, weak_secondary)
 
 
 if __name__ == "__main__":

@@ -96,7 +96,27 @@ struct gpmpc_handle {
     long long* stats = nullptr;            // optional per-instance solver statistics accumulators
     int32_t* scratch_i = nullptr;   // [2][max_batch]
     double* scratch_d = nullptr;    // [max_batch][4]
+    // the batch whose tightening variances the last solve's variance launch wrote into `var`
+    // (0: the last solve ran none, var is stale or unset)
+    int var_batch = 0;
+    // stream of the last call that queued work on the handle's device state; a call on another
+    // stream first waits for it (order_after_last), so consecutive calls never overlap
+    hipStream_t last_stream = nullptr;
+    bool last_stream_valid = false;
 };
+
+// The handle's device state (iterate, multipliers, variances, dispatch order) is read and written
+// by every queued call, so calls on different streams must not overlap: when the stream changes,
+// the new call waits for the previous stream's work (host synchronisation, only on a change).
+static hipError_t order_after_last(gpmpc_handle* h, hipStream_t s) {
+    if (h->last_stream_valid && h->last_stream != s) {
+        const hipError_t e = hipStreamSynchronize(h->last_stream);
+        if (e != hipSuccess) return e;
+    }
+    h->last_stream = s;
+    h->last_stream_valid = true;
+    return hipSuccess;
+}
 
 static hipEvent_t take_event(gpmpc_handle* h) {
     if (!h->ev_pool.empty()) {
@@ -215,10 +235,10 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     {
         const char* ev = std::getenv("GPMPC_LIN_CACHE");   // "0": recompute every linearisation (A/B)
         h->lin_cache = !(ev && ev[0] == '0');
-        const char* ec = std::getenv("GPMPC_CONDENSE");    // "1": condensed stage pairs (A/B)
-        P.condense = (ec && ec[0] == '1') ? 1 : 0;
-        const char* ew = std::getenv("GPMPC_WAVES");       // "1" / "4": waves per instance (A/B)
+        const char* ew = std::getenv("GPMPC_WAVES");       // "1" / "2" / "4": waves per instance (A/B)
         P.waves = ew ? std::atoi(ew) : 0;
+        if (P.waves != 1 && P.waves != 2 && P.waves != 4) P.waves = 0;
+        if (model_id == kQuad3D) P.waves = 0;             // quad3d always runs its four waves
         const char* eo = std::getenv("GPMPC_ORDER");       // "0": dispatch in instance order (A/B)
         P.order_dispatch = (eo && eo[0] == '0') ? 0 : 1;
         int ncu = 0;
@@ -357,6 +377,7 @@ gpmpc_status gpmpc_set_gp(gpmpc_handle* h, int32_t gp_id, int32_t n, int32_t d, 
         *p = nullptr;
     }
     h->gp_vroot_cols[gp_id] = 0;
+    h->gp_vroot_rank[gp_id] = 0;
     HIPCHK(hipMalloc(&h->gp_rows[gp_id], rows.size() * sizeof(double)));
     HIPCHK(hipMemcpy(h->gp_rows[gp_id], rows.data(), rows.size() * sizeof(double), hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&h->gp_tiles[gp_id], tiles.size() * sizeof(double)));
@@ -406,12 +427,16 @@ gpmpc_status gpmpc_set_gp_variance_root(gpmpc_handle* h, int32_t gp_id, int32_t 
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     if (gp_id < 0 || gp_id >= h->md.ngp) return fail(GPMPC_ERR_ARG, "gp_id out of range");
     (void)hipSetDevice(h->device);
-    if (h->gp_vroot[gp_id]) {
-        (void)hipFree(h->gp_vroot[gp_id]);
+    auto drop = [&]() {   // back to the exact variance: root, columns and rank together
+        if (h->gp_vroot[gp_id]) (void)hipFree(h->gp_vroot[gp_id]);
         h->gp_vroot[gp_id] = nullptr;
         h->gp_vroot_cols[gp_id] = 0;
+        h->gp_vroot_rank[gp_id] = 0;
+    };
+    if (!R) {
+        drop();
+        return GPMPC_OK;
     }
-    if (!R) return GPMPC_OK;   // back to the exact variance
     if (h->gp_npad[gp_id] == 0) return fail(GPMPC_ERR_STATE, "gpmpc_set_gp first");
     if (n != h->P.gp[gp_id].nv) return fail(GPMPC_ERR_ARG, "root rows must equal the variance GP's training rows");
     if (r < 1 || r > 16 * 16) return fail(GPMPC_ERR_ARG, "root rank must be 1..256");
@@ -419,8 +444,16 @@ gpmpc_status gpmpc_set_gp_variance_root(gpmpc_handle* h, int32_t gp_id, int32_t 
     std::vector<double> rp((size_t)npad * rpad, 0.0);
     for (int i = 0; i < n; ++i)
         for (int c = 0; c < r; ++c) rp[(size_t)i * rpad + c] = R[(size_t)i * r + c];
-    HIPCHK(hipMalloc(&h->gp_vroot[gp_id], rp.size() * sizeof(double)));
-    HIPCHK(hipMemcpy(h->gp_vroot[gp_id], rp.data(), rp.size() * sizeof(double), hipMemcpyHostToDevice));
+    // staged in a local buffer: the handle's root, columns and rank change together, on success only
+    double* buf = nullptr;
+    hipError_t e = hipMalloc(&buf, rp.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(buf, rp.data(), rp.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (buf) (void)hipFree(buf);
+        return fail(GPMPC_ERR_HIP, std::string("LOVE root upload: ") + hipGetErrorString(e));
+    }
+    drop();
+    h->gp_vroot[gp_id] = buf;
     h->gp_vroot_cols[gp_id] = rpad;
     h->gp_vroot_rank[gp_id] = r;
     return GPMPC_OK;
@@ -501,6 +534,7 @@ gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, 
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
+    HIPCHK(order_after_last(h, s));
     HIPCHK(hipMemsetAsync(h->has_prev, 0, B * sizeof(int32_t), s));
     bump_lin(h);
     if (reset_iterate) {
@@ -510,6 +544,7 @@ gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, 
         HIPCHK(hipMemsetAsync(h->lam, 0, B * (H + 1) * 2 * h->nb * sizeof(double), s));
     }
     if (batch == h->max_batch) h->any_prev = false;
+    h->var_batch = 0;
     return GPMPC_OK;
 }
 
@@ -519,6 +554,7 @@ gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_d
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
+    HIPCHK(order_after_last(h, s));
     HIPCHK(hipMemcpyAsync(h->x, x_dev, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->u, u_dev, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
     bump_lin(h);
@@ -539,15 +575,23 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             if (!h->gp_linvT[g]) return fail(GPMPC_ERR_STATE, "tightening needs Linv for every GP");
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
+    HIPCHK(order_after_last(h, s));
     ProblemDev P = h->P;
     P.tighten = (h->P.tighten && h->P.use_gp) ? 1 : 0;
+    // Profiling events are best effort: a failed record drops that launch's timing (the events go
+    // back to the pool), never the solve.  Every early return below recycles what it took.
+    auto give_back = [&](hipEvent_t& e) {
+        if (e) h->ev_pool.push_back(e);
+        e = nullptr;
+    };
     // 1. GP variances at the previous solution (the MFMA contraction), only when needed
     hipEvent_t e0 = nullptr, e1 = nullptr, mid = nullptr;
-    if (P.tighten && h->any_prev) {
+    const bool var_launch = P.tighten && h->any_prev;
+    if (var_launch) {
         if (h->profiling) {
             e0 = take_event(h);
             e1 = take_event(h);
-            if (e0) HIPCHK(hipEventRecord(e0, s));
+            if (e0 && hipEventRecord(e0, s) != hipSuccess) give_back(e0);
         }
         PostBatch pb{};
         pb.n = h->md.ngp;
@@ -574,16 +618,22 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             pb.g[g].vroot_rank = h->gp_vroot_rank[g];
             pb.npad[g] = h->gp_npad[g];
         }
-        HIPCHK(launch_gp_post_batch(pb, true, s));
-        if (e0 && e1) {
-            HIPCHK(hipEventRecord(e1, s));
+        const hipError_t ve = launch_gp_post_batch(pb, true, s);
+        if (ve != hipSuccess) {
+            give_back(e0);
+            give_back(e1);
+            h->var_batch = 0;
+            return fail(GPMPC_ERR_HIP, std::string("launch_gp_post_batch: ") + hipGetErrorString(ve));
+        }
+        if (e0 && e1 && hipEventRecord(e1, s) == hipSuccess) {
             h->ev_var.push_back({e0, e1});
             mid = e1;   // also the SQP launch's start
         } else {
-            if (e0) h->ev_pool.push_back(e0);
-            if (e1) h->ev_pool.push_back(e1);
+            give_back(e0);
+            give_back(e1);
         }
     }
+    h->var_batch = var_launch ? batch : 0;
     // 2. the SQP step
     StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag,
                h->order, h->cost};
@@ -597,9 +647,10 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         e0 = mid;
         if (!e0) {
             e0 = take_event(h);
-            if (e0) HIPCHK(hipEventRecord(e0, s));
+            if (e0 && hipEventRecord(e0, s) != hipSuccess) give_back(e0);
         }
         e1 = take_event(h);
+        if (!e0) give_back(e1);
     }
     // events not handed to ev_sqp: the shared `mid` stays in use as ev_var's end event (the
     // variance list takes ownership of it), the others go back to the pool, on every exit path
@@ -608,33 +659,39 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         else if (e0) h->ev_pool.push_back(e0);
         if (e1) h->ev_pool.push_back(e1);
     };
-    hipError_t le = launch_sqp(P, S, io, batch, s);
-    if (le == hipSuccess && e0 && e1) le = hipEventRecord(e1, s);
+    const hipError_t le = launch_sqp(P, S, io, batch, s);
     if (le != hipSuccess) {
         recycle();
         return fail(GPMPC_ERR_HIP, std::string("launch_sqp: ") + hipGetErrorString(le));
     }
-    if (e0 && e1) h->ev_sqp.push_back({e0, e1});
-    else recycle();
+    // the SQP kernel is queued and will update the iterate: from here on the host state follows it
     h->any_prev = true;
+    if (e0 && e1 && hipEventRecord(e1, s) == hipSuccess) h->ev_sqp.push_back({e0, e1});
+    else recycle();   // lost profiling data only
     return GPMPC_OK;
 }
 
 gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev, void* stream) {
     if (!h || !var_dev) return fail(GPMPC_ERR_ARG, "null argument");
     if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    if (h->var_batch == 0)
+        return fail(GPMPC_ERR_STATE, "the last solve ran no variance launch (first step, tightening or GPs off)");
+    if (batch > h->var_batch)
+        return fail(GPMPC_ERR_ARG, "the last variance launch covered " + std::to_string(h->var_batch) + " instances");
     (void)hipSetDevice(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(order_after_last(h, s));
     const size_t B = batch, H = h->H;
-    HIPCHK(hipMemcpyAsync(var_dev, h->var, B * H * h->md.ngp * sizeof(double), hipMemcpyDeviceToDevice,
-                          (hipStream_t)stream));
+    HIPCHK(hipMemcpyAsync(var_dev, h->var, B * H * h->md.ngp * sizeof(double), hipMemcpyDeviceToDevice, s));
     return GPMPC_OK;
 }
 
-gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves, int32_t condense) {
+gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     if (waves != 0 && waves != 1 && waves != 2 && waves != 4) return fail(GPMPC_ERR_ARG, "waves must be 0 (auto), 1, 2 or 4");
+    if (h->model == kQuad3D && waves != 0 && waves != 4)
+        return fail(GPMPC_ERR_ARG, "quad3d runs four waves per instance (waves must be 0 or 4)");
     h->P.waves = waves;
-    h->P.condense = condense ? 1 : 0;
     return GPMPC_OK;
 }
 
@@ -730,6 +787,7 @@ gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, d
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
+    HIPCHK(order_after_last(h, s));
     if (x_dev) HIPCHK(hipMemcpyAsync(x_dev, h->x, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (u_dev) HIPCHK(hipMemcpyAsync(u_dev, h->u, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (tight_dev)

@@ -79,9 +79,8 @@ struct ProblemDev {
     // linearisation depends on (iterate, GPs, model parameters, GP switch); 0 disables the cache
     int32_t lin_gen;
     // launch shape of the SQP kernel: waves per instance (0: auto -- four when batch <= n_cu for the
-    // single-tile models, sqp_kernel.hip sqp_waves), two-stage condensed recursions (H even)
+    // single-tile models, sqp_kernel.hip sqp_waves)
     int32_t waves;
-    int32_t condense;
     int32_t n_cu;             // compute units of the device (set by gpmpc_create)
     // cost-ordered dispatch (StateDev::order): on when a launch has more instances than the
     // device holds at once (GPMPC_ORDER=0 turns it off, for A/B)

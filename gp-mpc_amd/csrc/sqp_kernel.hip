@@ -300,19 +300,11 @@ struct SqpKernel {
     // Riccati on v_mfma_f64_16x16x4 when every stage product fits one 16x16 tile
     // (G' has NB+1 <= 16 columns, the forward state [dx; 1] has NX+1 <= 8 rows).
     static constexpr bool kMfma = (NB + 1 <= 16) && (NX + 1 <= 8);
-    // Two-stage condensing of the Newton systems (kCond, H even): stage pairs (2j, 2j + 1) become
-    // one block with state x_2j and inputs [u_2j; u_2j+1] (NCU <= 4 tile slots), so the sequential
-    // Riccati factorisation and sweeps run over H/2 blocks (cond_backward and the sweeps below).
-    static constexpr int NCU = 2 * NU;
-    static constexpr bool kCond = kMfma && NCU <= 4;
-    // stages per block of the Newton-system recursions for horizon H (1: stage by stage)
-    __host__ __device__ static constexpr int cf_of(int H) { return (kCond && H % 2 == 0) ? 2 : 1; }
     // multipliers kept in LDS during the step when the layout has room for them (single-tile models on
     // four waves: one instance per CU); otherwise they stay in global memory (rows read / written per
     // SQP iteration).  quad3d keeps them global: its LDS copy measured 4.6 % slower at config 5 (the
     // 14 KB push its 140 KB layout further and the copies sit on the step's critical path).
-    __host__ __device__ static constexpr bool lds_mult(int CF) { return NW > 1 && kMfma; }
-    static constexpr int GH = NX + 1 + NCU;   // row of the condensed dynamics G^_j: [G^_x | c^ | G^_u]
+    static constexpr bool lds_mult = NW > 1 && kMfma;
     // Waves per instance.  The wide model (quad3d) needs more LDS than two instances per CU can
     // have, so its CU's other SIMDs would idle: three GP helper waves take a share of every GP
     // tile pass (gp_tiles over tiles w, w + 4, ...) and of the IPM's elementwise work (WSPL), the
@@ -327,8 +319,6 @@ struct SqpKernel {
     struct Lds {
         double *G, *P, *K, *Rui, *hq, *gq, *dxv, *cd, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
         double *Dq, *xs;             // WSPL: step-vector exchange, reduction slots
-        double *Gh, *dpv, *Tc;       // condensed blocks (CF = 2): G^_j rows, dpi of every stage (and
-                                     // the corrector's block gradients), corrector scratch t_j
         double *lam, *pim;           // the instance's multipliers during the step (acados memory):
                                      // bounds [H+1][2 NB], dynamics [H][NX]
         int* ctrl;   // GP helper command (NWAVES > 1): GP index of the next tile pass, -1 = exit
@@ -342,80 +332,62 @@ struct SqpKernel {
         // + the helper waves' partial sums [NWAVES-1][16*NE][4]
         return (size_t)9 * NGP * 16 * ((H + 15) / 16) + (size_t)(NWAVES - 1) * 64 * ((H + 15) / 16);
     }
-    // P' at the block boundaries (+ the corrector scratch Tc when condensed) | GP scratch
-    __host__ __device__ static size_t p_region(int H, int CF) {
-        const int HB = H / CF;
-        const size_t pp = (size_t)(HB + 1) * PP + (CF == 2 ? (size_t)HB * NX : 0);
+    // P'_k of every stage boundary | GP scratch
+    __host__ __device__ static size_t p_region(int H) {
+        const size_t pp = (size_t)(H + 1) * PP;
         return pp > gp_scratch(H) ? pp : gp_scratch(H);
     }
-    __host__ __device__ static size_t lds_doubles(int H, int CF) {
-        const int HB = H / CF, NK = CF * NU;   // blocks of the recursions, their inputs
+    __host__ __device__ static size_t lds_doubles(int H) {
         const size_t common = (size_t)64                     // dummy store slots (branch-free stores)
                               + (size_t)8                    // zero slots (branch-free masked loads)
                               + (size_t)8                    // GP helper command slot
-                              + (lds_mult(CF) ? (size_t)(H + 1) * 2 * NB + (size_t)H * NX : 0)   // multipliers
+                              + (lds_mult ? (size_t)(H + 1) * 2 * NB + (size_t)H * NX : 0)   // multipliers
                               + (size_t)H * NX * GS            // G'_k
-                              + (size_t)HB * NK * PS         // K'_j
-                              + (size_t)HB * NK * NK         // Ru_j^-1
+                              + (size_t)H * NU * PS          // K'_k
+                              + (size_t)H * NU * NU          // Ru_k^-1
                               + (size_t)(H + 1) * NB * 2     // hq, gq
-                              + (size_t)((NW > 1 || CF == 2 ? H : HB) + 1) * NX   // dx (forward sweep: block
-                                                                        // boundaries; condensed: every stage;
-                                                                        // WSPL: the published residual)
-                              + (CF == 2 ? (size_t)H * NX : 0);   // dpi of every stage
+                              + (size_t)(H + 1) * NX;        // dx (forward sweep; WSPL: the published residual)
         if (kMfma) {
-            // CF = 1: closed-loop A'_k; CF = 2: G^_j.  The tightening scratch aliases it, and (WSPL) the
-            // step-vector exchange Dq, which the condensed layout keeps apart (G^ lives through the QP).
-            const size_t acl = CF == 2 ? (size_t)HB * NX * GH : (size_t)HB * NX * PS;
-            return common + p_region(H, CF) + (acl > tight_scratch(H) ? acl : tight_scratch(H))
-                   + (NWAVES > 1 ? 64 + (CF == 2 ? (size_t)(H + 1) * NB : 0) : 0);   // WSPL: xs (+ Dq)
+            // closed-loop A'_k; the tightening scratch and (WSPL) the step-vector exchange Dq alias it
+            const size_t acl = (size_t)H * NX * PS;
+            return common + p_region(H) + (acl > tight_scratch(H) ? acl : tight_scratch(H))
+                   + (NWAVES > 1 ? 64 : 0);   // WSPL: xs
         }
-        return common + p_region(H, CF)                         // P'_k (packed) | GP scratch
+        return common + p_region(H)                             // P'_k (packed) | GP scratch
                + tight_scratch(H)
                + (NWAVES > 1 ? (size_t)(H + 1) * NB + 64 : 0);  // WSPL exchange (Dq, xs)
     }
-    template <int CF>
     __device__ static Lds carve(double* s, int H) {
-        const int HB = H / CF;
-        constexpr int NK = CF * NU;
         Lds L{};
         L.dummy = s; s += 64;
         L.zero = s;  s += 8;
         L.ctrl = reinterpret_cast<int*>(s);  s += 8;
-        if constexpr (lds_mult(CF)) {
+        if constexpr (lds_mult) {
             L.lam = s; s += (size_t)(H + 1) * 2 * NB;
             L.pim = s; s += (size_t)H * NX;
         }
         L.G = s;   s += (size_t)H * NX * GS;
-        L.K = s;   s += (size_t)HB * NK * PS;
-        L.Rui = s; s += (size_t)HB * NK * NK;
+        L.K = s;   s += (size_t)H * NU * PS;
+        L.Rui = s; s += (size_t)H * NU * NU;
         L.hq = s;  s += (size_t)(H + 1) * NB;
         L.gq = s;  s += (size_t)(H + 1) * NB;
-        L.dxv = s; s += (size_t)((NW > 1 || CF == 2 ? H : HB) + 1) * NX;
-        if constexpr (CF == 2) {
-            L.dpv = s; s += (size_t)H * NX;
-            L.Tc = s + (size_t)(HB + 1) * PP;   // behind the boundary P' blocks in the P region
-        }
+        L.dxv = s; s += (size_t)(H + 1) * NX;
         L.gz = s;
         L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         L.gs = L.gc + (size_t)NGP * 16 * ((H + 15) / 16);
         L.gsh = L.gs + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
         if (kMfma) {
-            L.P = s;   s += p_region(H, CF);
+            L.P = s;   s += p_region(H);
             L.Acl = s;
-            L.Gh = s;
             L.cd = s;
             if constexpr (NWAVES > 1) {   // Dq: live only inside an IPM iteration's residual phase
                 L.Dq = s;
-                const size_t acl = CF == 2 ? (size_t)HB * NX * GH : (size_t)HB * NX * PS;
+                const size_t acl = (size_t)H * NX * PS;
                 s += acl > tight_scratch(H) ? acl : tight_scratch(H);
-                if constexpr (CF == 2) {
-                    L.Dq = s;
-                    s += (size_t)(H + 1) * NB;
-                }
                 L.xs = s;
             }
         } else {
-            L.P = s;   s += p_region(H, CF);
+            L.P = s;   s += p_region(H);
             L.cd = s;  s += tight_scratch(H);
             if constexpr (NWAVES > 1) {
                 L.Dq = s;  s += (size_t)(H + 1) * NB;
@@ -967,565 +939,6 @@ struct SqpKernel {
         return ok;
     }
 
-    // ------------------------------------------------------------------ condensed Riccati (kCond, H even)
-    // Block j = stages k0 = 2j, k1 = 2j + 1 with the block input z = [x_k0; u_k0; u_k1; 1] in the tile
-    // layout x_t (t < NX), CI = NX, u_k0 at UI .. UI+NU-1, u_k1 at UI+NU .. UI+NCU-1 (UI = 8).  With
-    // T = [G'_k0; e_CI] (x_k1 = T z) and the condensed dynamics x_2j+2 = G^_j z,
-    //   G^_j = A_k1 T + B_k1 (u_k1 slots) + c_k1 e_CI^T        (stored per block: [G^_x | c^ | G^_u]),
-    // the block's cost-to-go is  M = G^''^T P'_{j+1} G^'' + E_A^T E_B + D^  with (tile rows 8 + m, m < NX)
-    //   E_A = diag(h) T + g e_CI^T,  E_B = T + diag(g / h) e_CI^T        (h, g: hq, gq of x_k1),
-    // so E_A^T E_B = T^T diag(h) T plus the gradient terms in row/column CI (the (CI, CI) entry is a
-    // constant of the cost-to-go, never read), and D^ the diagonal / gradient of x_k0, u_k0, u_k1.
-    // On v_mfma_f64_16x16x4: W = P' G^'' (2 MFMAs), M = G^''^T W over K-steps 0..1 on top of
-    // E_A^T E_B + D^ (K-steps 2..3 of the stacked system [P' 0; 0 I], whose operands are E_A / E_B),
-    // then Ru = M_uu (NCU x NCU), K^' = -Ru^-1 M_u and P'_j = M + M_.u K^' (1 MFMA) as in
-    // mfma_backward_h: five dependent MFMA links per block instead of ten per stage pair.  The next
-    // block's operands are 11 LDS loads issued behind the W products; its E^T E products run on the
-    // matrix core while the VALU forms Ru^-1.  Outputs: packed P' at the block boundaries,
-    // K^'_j = [K^ | kff^] (NCU rows), Ru_j^-1 (NCU x NCU).
-    // Everything else of the Newton solve works on G^ without forming the closed-loop maps:
-    // A^_j = [G^_x + G^_u K^_j | c^ + G^_u kff^_j] enters the 4-block MFMA sweeps entry by entry.
-
-    // G^_j rows (one (j, r) per lane and pass).  withx: all columns (once per SQP iteration: G^_x and
-    // G^_u depend on the linearisation only); otherwise the affine column c^ (every IPM iteration:
-    // c_k is the current dynamics residual, column NB of G').
-    template <bool withx>
-    __device__ static void cond_ghat(const Lds& L, int H, int lane) {
-        const int HB = H >> 1;
-        for (int e = lane; e < HB * NX; e += 64) {
-            const int j = e / NX, r = e - j * NX;
-            const double* G0 = L.G + (size_t)(2 * j) * NX * GS;
-            const double* g1 = G0 + NX * GS + r * GS;
-            double a1[NX];
-#pragma unroll
-            for (int m = 0; m < NX; ++m) a1[m] = g1[m];
-            auto col = [&](int c) {
-                double acc = 0.0;
-#pragma unroll
-                for (int m = 0; m < NX; ++m) acc = fma(a1[m], G0[m * GS + c], acc);
-                return acc;
-            };
-            double* out = L.Gh + (size_t)e * GH;
-            if constexpr (withx) {
-                double o[GH];
-#pragma unroll
-                for (int c = 0; c < NX; ++c) o[c] = col(c);
-                o[NX] = col(NB) + g1[NB];
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    o[NX + 1 + a] = col(NX + a);
-                    o[NX + 1 + NU + a] = g1[NX + a];
-                }
-#pragma unroll
-                for (int c = 0; c < GH; ++c) out[c] = o[c];
-            } else {
-                out[NX] = col(NB) + g1[NB];
-            }
-        }
-    }
-
-    __device__ static bool cond_backward(const Lds& L, int H, int lane) {
-        if constexpr (!kCond) {
-            return false;
-        } else {
-        const int lr = lane >> 4, lc = lane & 15;
-        constexpr int CI = NX, UI = 8;
-        static_assert(NX + 1 <= 8 && UI + NCU <= 12 && UI + NX <= 16, "condensed tile layout");
-        const int HB = H >> 1;
-        // tile column lc: the G' column of T = G''_k0 it reads and the G^ column (-1: none)
-        const int gc0 = lc < NX ? lc : (lc == CI ? NB : ((lc >= UI && lc < UI + NU) ? NX + lc - UI : -1));
-        const int hc = lc < NX ? lc : (lc == CI ? NX : ((lc >= UI && lc < UI + NCU) ? NX + 1 + lc - UI : -1));
-        // block variable of tile slot t: (stage offset i, stage variable v), or v = -1
-        auto bvar = [](int t, int& i) {
-            i = 0;
-            if (t < NX) return t;
-            if (t >= UI && t < UI + NCU) { i = (t - UI) / NU; return NX + (t - UI) % NU; }
-            return -1;
-        };
-        double pn[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {   // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
-            const int t = lr + 4 * r;
-            double v = 0.0;
-            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
-            else if (t < NX && lc == CI) v = L.gq[H * NB + t];
-            else if (t == CI && lc < NX) v = L.gq[H * NB + lc];
-            pn[r] = v;
-        }
-        {   // P'_H (packed, boundary HB) for the multipliers of stage H-1
-            double* PH = L.P + (size_t)HB * PP;
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int t = lr + 4 * r;
-                if (t < NX) {
-                    if (lc == CI) PH[PO + t] = pn[r];
-                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
-                }
-            }
-        }
-        bool ok = true;
-        // operand streams, blocks HB-1 .. 0 (masked entries read the zero / one slots with stride 0)
-        const double* pg[2];    // G^'' rows lr + 4q, column lc
-        const double* pt[2];    // T rows m = lr + 4q, column lc
-        const double* ph[2];    // hq, gq of x_k1[m]
-        const double* pq[2];
-        int gst[2], tst[2], hst[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int r = lr + 4 * q;
-            const bool ld = r < NX && hc >= 0, one = r == CI && lc == CI;
-            pg[q] = ld ? L.Gh + ((size_t)(HB - 1) * NX + r) * GH + hc : L.zero + (one ? 7 : 0);
-            gst[q] = ld ? NX * GH : 0;
-            const bool lt = r < NX && gc0 >= 0;
-            pt[q] = lt ? L.G + (size_t)(2 * HB - 2) * NX * GS + r * GS + gc0 : L.zero;
-            tst[q] = lt ? 2 * NX * GS : 0;
-            const bool lh = r < NX;
-            ph[q] = lh ? L.hq + (size_t)(2 * HB - 1) * NB + r : L.zero + 7;   // masked: h = 1, g = 0
-            pq[q] = lh ? L.gq + (size_t)(2 * HB - 1) * NB + r : L.zero;
-            hst[q] = lh ? 2 * NB : 0;
-        }
-        const double* pd[3];   // D^ (rows lr + 4r, r = 0..2)
-        int dst[3];
-        int ilc;
-        const int vlc = bvar(lc, ilc);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int t = lr + 4 * r;
-            int it;
-            const int vt = bvar(t, it);
-            const double* base = L.zero;
-            bool on = false;
-            if (vt >= 0 && t == lc) { base = L.hq + it * NB + vt; on = true; }
-            else if (vt >= 0 && lc == CI) { base = L.gq + it * NB + vt; on = true; }
-            else if (t == CI && vlc >= 0) { base = L.gq + ilc * NB + vlc; on = true; }
-            pd[r] = on ? base + (size_t)(2 * HB - 2) * NB : L.zero;
-            dst[r] = on ? 2 * NB : 0;
-        }
-        struct Raw { double g[2], t[2], h[2], q[2], d[3]; };
-        struct Blk { double g[2]; f64x4 mb; };
-        auto load = [&](Raw& rw) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                rw.g[q] = *pg[q];
-                pg[q] -= gst[q];
-                rw.t[q] = *pt[q];
-                pt[q] -= tst[q];
-                rw.h[q] = *ph[q];
-                ph[q] -= hst[q];
-                rw.q[q] = *pq[q];
-                pq[q] -= hst[q];
-            }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                rw.d[r] = *pd[r];
-                pd[r] -= dst[r];
-            }
-        };
-        // E_A, E_B rows (VALU) and E_A^T E_B + D^ (K-steps 2, 3 of M: independent of P', 2 MFMAs)
-        const unsigned mci = lc == CI ? ~0u : 0u;
-        struct Eop { double a[2], b[2], d[3]; };
-        auto make_e = [&](const Raw& rw, Blk& bk, Eop& eo) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const double gi = rw.q[q] * fast_rcp(rw.h[q]);
-                eo.a[q] = fma(rw.h[q], rw.t[q], bsel(mci, rw.q[q], 0.0));
-                eo.b[q] = rw.t[q] + bsel(mci, gi, 0.0);
-                bk.g[q] = rw.g[q];
-            }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) eo.d[r] = rw.d[r];
-        };
-        auto make_mb = [&](const Eop& eo, Blk& bk) {
-            bk.mb = mfma64(eo.a[0], eo.b[0], f64x4{eo.d[0], eo.d[1], eo.d[2], 0.0});
-            bk.mb = mfma64(eo.a[1], eo.b[1], bk.mb);
-        };
-        // store streams (blocks HB-1 .. 0), dummy slot with stride 0 for entries not stored
-        double* sp[2];
-        int sp_st[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int t = lr + 4 * r;
-            const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc));
-            const int idx = (lc == CI) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
-            sp[r] = st ? L.P + (size_t)(HB - 1) * PP + idx : L.dummy + lane;
-            sp_st[r] = st ? PP : 0;
-        }
-        const bool kst = lr < NCU && (lc < NX || lc == CI);
-        double* sk = kst ? L.K + (size_t)(HB - 1) * NCU * PS + lr * PS + (lc == CI ? NX : lc) : L.dummy + lane;
-        const int sk_st = kst ? NCU * PS : 0;
-        const bool rst = lr < NCU && lc < NCU;
-        double* srui = rst ? L.Rui + (size_t)(HB - 1) * NCU * NCU + lr * NCU + lc : L.dummy + lane;
-        const int srui_st = rst ? NCU * NCU : 0;
-        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
-        bool pend = false;
-        auto flush = [&]() {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                *sp[r] = pend_p[r];
-                sp[r] -= sp_st[r];
-            }
-            *sk = pend_k;
-            sk -= sk_st;
-            *srui = pend_r;
-            srui -= srui_st;
-        };
-        // one block: the chain W -> M -> Ru^-1 -> Schur.  The next block's loads are issued behind
-        // the W products, its E operands formed in the shadow of the M products, and its two
-        // E_A^T E_B MFMAs issued right after M (the matrix core idles while the VALU forms Ru^-1)
-        Raw rw;
-        Eop eo;
-        const unsigned ma0 = lr == 0 ? ~0u : 0u, ma1 = lr == 1 ? ~0u : 0u, ma2 = lr == 2 ? ~0u : 0u;
-        const unsigned mb1 = (lr & 2) ? ~0u : 0u, mb2 = (lr & 1) ? ~0u : 0u, mb3 = ((lr ^ (lr >> 1)) & 1) ? ~0u : 0u;
-        const int tsel = lc ^ lr;
-        const unsigned mt0 = tsel == 0 ? ~0u : 0u, mt1 = tsel == 1 ? ~0u : 0u, mt2 = tsel == 2 ? ~0u : 0u;
-        const unsigned ml0 = lane == 0 ? ~0u : 0u, ml17 = lane == 17 ? ~0u : 0u, mlu = lr < NCU ? ~0u : 0u;
-        auto block = [&](const Blk& cb, Blk& nb, bool more) {
-            f64x4 w = mfma64(pn[0], cb.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
-            w = mfma64(pn[1], cb.g[1], w);
-            __builtin_amdgcn_sched_barrier(0);
-            if (pend) flush();
-            pend = true;
-            if (more) load(rw);
-            __builtin_amdgcn_sched_barrier(0);
-            f64x4 m = mfma64(cb.g[0], w[0], cb.mb);
-            m = mfma64(cb.g[1], w[1], m);
-            __builtin_amdgcn_sched_barrier(0);
-            if (more) {
-                make_e(rw, nb, eo);
-                make_mb(eo, nb);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            const double mu = m[2];          // lane (q, c) <- M[UI + q][c]
-            double kb, rv;
-            if constexpr (NCU == 2) {
-                const double r00 = readlane_d(mu, UI), r01 = readlane_d(mu, UI + 1), r11 = readlane_d(mu, 16 + UI + 1);
-                const double det = r00 * r11 - r01 * r01;
-                ok = ok && (r00 > 0.0) && (det > 0.0);
-                const double mo = xor16_d(mu);
-                const double num = fma((lr & 1) ? r00 : r11, mu, -r01 * mo);   // adj(Ru) M_u
-                const double r0 = __builtin_amdgcn_rcp(det);
-                const double e = fma(-det, r0, 1.0);
-                const double ee = fma(e, e, e);
-                const double t = num * -r0;
-                const double id = fma(r0, ee, r0);
-                kb = fma(t, ee, t);
-                rv = bsel(ml0, r11 * id, bsel(ml17, r00 * id, -r01 * id));
-            } else {
-                // Ru^-1 by 2x2 blocks [[A, B], [B^T, C]] (as mfma_backward_big)
-                const double a00 = readlane_d(mu, UI), a01 = readlane_d(mu, UI + 1), a11 = readlane_d(mu, 16 + UI + 1);
-                const double b00 = readlane_d(mu, UI + 2), b01 = readlane_d(mu, UI + 3), b10 = readlane_d(mu, 16 + UI + 2),
-                             b11 = readlane_d(mu, 16 + UI + 3);
-                const double c00 = readlane_d(mu, 32 + UI + 2), c01 = readlane_d(mu, 32 + UI + 3),
-                             c11 = readlane_d(mu, 48 + UI + 3);
-                const double dA = fma(a00, a11, -a01 * a01);
-                const double iA = fast_rcp(dA);
-                const double A00 = a11 * iA, A01 = -a01 * iA, A11 = a00 * iA;
-                const double X00 = fma(A00, b00, A01 * b10), X01 = fma(A00, b01, A01 * b11);
-                const double X10 = fma(A01, b00, A11 * b10), X11 = fma(A01, b01, A11 * b11);
-                const double S00 = c00 - fma(b00, X00, b10 * X10), S01 = c01 - fma(b00, X01, b10 * X11);
-                const double S11 = c11 - fma(b01, X01, b11 * X11);
-                const double dS = fma(S00, S11, -S01 * S01);
-                ok = ok && (a00 > 0.0) && (dA > 0.0) && (dS > 0.0);
-                const double iS = fast_rcp(dS);
-                const double C00 = S11 * iS, C01 = -S01 * iS, C11 = S00 * iS;
-                const double Y00 = fma(X00, C00, X01 * C01), Y01 = fma(X00, C01, X01 * C11);
-                const double Y10 = fma(X10, C00, X11 * C01), Y11 = fma(X10, C01, X11 * C11);
-                const double Z00 = A00 + fma(Y00, X00, Y01 * X01), Z01 = A01 + fma(Y00, X10, Y01 * X11);
-                const double Z11 = A11 + fma(Y10, X10, Y11 * X11);
-                // Ru^-1 = [[Z, -Y], [-Y^T, C]]; row a = lr, column a ^ t (branch-free lane selects)
-                const double c0 = bsel(ma0, Z00, bsel(ma1, Z11, bsel(ma2, C00, C11)));
-                const double c1 = bsel(mb1, C01, Z01);
-                const double c2 = bsel(mb2, -Y11, -Y00);
-                const double c3 = bsel(mb3, -Y10, -Y01);
-                const double v1 = xor16_d(mu), v2 = xor32_d(mu), v3 = xor32_d(v1);   // rows UI + (a ^ 1, 2, 3)
-                kb = -fma(c0, mu, fma(c1, v1, fma(c2, v2, c3 * v3)));
-                rv = bsel(mt0, c0, bsel(mt1, c1, bsel(mt2, c2, c3)));
-            }
-            const f64x4 pk = mfma64(bsel(mlu, mu, 0.0), kb, m);   // P'_j = M + M_.u K^'
-            pend_p[0] = pk[0];
-            pend_p[1] = pk[1];
-            pend_k = kb;
-            pend_r = rv;
-            pn[0] = pk[0];
-            pn[1] = pk[1];
-        };
-        Blk b0, b1;
-        load(rw);
-        make_e(rw, b0, eo);
-        make_mb(eo, b0);
-        int j = HB - 1;
-        for (; j >= 1; j -= 2) {   // two blocks per iteration (ping-pong: no register copies)
-            block(b0, b1, true);
-            block(b1, b0, j >= 2);
-        }
-        if (j == 0) block(b0, b1, false);
-        flush();
-        return ok;
-        }
-    }
-
-    // One entry of the closed-loop block map A^_j = [G^_x + G^_u K^_j | c^ + G^_u kff^_j] for the
-    // 4-block sweeps: row r, column c (c = NX: the affine column), from G^_j and K^_j.
-    struct CondOp { double g, b[NCU], k[NCU]; };
-    __device__ static void cond_op_load(const double* gr, const double* kc, int c, CondOp& op) {
-        op.g = gr[c];
-#pragma unroll
-        for (int q = 0; q < NCU; ++q) {
-            op.b[q] = gr[NX + 1 + q];
-            op.k[q] = kc[q * PS];
-        }
-    }
-    __device__ static double cond_op(const CondOp& op) {
-        double acc = op.g;
-#pragma unroll
-        for (int q = 0; q < NCU; ++q) acc = fma(op.b[q], op.k[q], acc);
-        return acc;
-    }
-
-    // Forward sweep over the blocks: dx_2j+2 = A^_j [dx_2j; 1] on the 4-block MFMA (mfma4_stage), the
-    // stage operand A^_j[row][col] formed from G^_j and K^_j a block ahead; dx at the boundaries.
-    __device__ static void cond_forward(const Lds& L, int H, int lane) {
-        const int HB = H >> 1;
-        const Mfma4Lane q = mfma4_lane(lane);
-        const bool ld = q.row < NX && q.col <= NX;
-        const bool one = q.row == NX && q.col == NX;
-        const double* gr = L.Gh + (size_t)(ld ? q.row : 0) * GH;   // row of G^_j (stride NX GH per block)
-        const double* kc = L.K + (ld ? q.col : 0);                  // column of K^_j (stride NCU PS)
-        const int gcol = q.col < NX ? q.col : NX;
-        const int gs = ld ? NX * GH : 0, ks = ld ? NCU * PS : 0;
-        const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
-        const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
-        double* out = stlo ? L.dxv + 2 * NX + q.r : (sthi ? L.dxv + 2 * NX + 4 + q.r : L.dummy + lane);
-        const int ost = (stlo || sthi) ? 2 * NX : 0;
-        if (lane < NX) L.dxv[lane] = 0.0;
-        double y = mfma4_vec(q, [](int) { return 0.0; });
-        CondOp o0, o1;
-        cond_op_load(gr, kc, gcol, o0);
-        auto step = [&](const CondOp& op) {
-            const double a = ld ? cond_op(op) : (one ? 1.0 : 0.0);
-            double sv;
-            y = mfma4_stage(a, y, sv);
-            *out = sv;
-            out += ost;
-        };
-        int j = 0;
-        for (; j + 1 < HB; j += 2) {
-            gr += gs;
-            kc += ks;
-            cond_op_load(gr, kc, gcol, o1);
-            step(o0);
-            if (j + 2 < HB) {
-                gr += gs;
-                kc += ks;
-                cond_op_load(gr, kc, gcol, o0);
-            }
-            step(o1);
-        }
-        if (j < HB) step(o0);
-    }
-
-    // Interior states and every stage's dynamics multipliers from the boundary states (all entries
-    // in parallel): dx_2j+1 = A_k0 dx_2j + B_k0 du_k0 + c_k0 (du_k0 = K^_j rows 0..NU-1 [dx_2j; 1]),
-    // dpi_2j+1 = -(P_{j+1} dx_2j+2 + p_{j+1}), then
-    // dpi_2j = A_k1^T dpi_2j+1 - hq_k1,x dx_2j+1 - gq_k1,x (stationarity at x_k1).
-    __device__ static void cond_expand(const Lds& L, int H, int lane) {
-        const int HB = H >> 1, n = HB * NX;
-        for (int e = lane; e < 2 * n; e += 64) {
-            const int f = e < n ? e : e - n, j = f / NX, i = f - j * NX;
-            if (e < n) {
-                const double* x0 = L.dxv + (size_t)(2 * j) * NX;
-                const double* Kj = L.K + (size_t)j * NCU * PS;
-                const double* g0 = L.G + (size_t)(2 * j) * NX * GS + i * GS;
-                double xv[NX];
-#pragma unroll
-                for (int c = 0; c < NX; ++c) xv[c] = x0[c];
-                double acc = g0[NB];
-#pragma unroll
-                for (int c = 0; c < NX; ++c) acc = fma(g0[c], xv[c], acc);
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    double du = Kj[a * PS + NX];
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) du = fma(Kj[a * PS + c], xv[c], du);
-                    acc = fma(g0[NX + a], du, acc);
-                }
-                L.dxv[(size_t)(2 * j + 1) * NX + i] = acc;
-            } else {
-                const double* Pn = L.P + (size_t)(j + 1) * PP;
-                const double* xn = L.dxv + (size_t)(2 * j + 2) * NX;
-                double acc = Pn[PO + i];
-#pragma unroll
-                for (int c = 0; c < NX; ++c) acc = fma(Pn[i <= c ? pidx(i, c) : pidx(c, i)], xn[c], acc);
-                L.dpv[(size_t)(2 * j + 1) * NX + i] = -acc;
-            }
-        }
-        WSYNC();
-        for (int e = lane; e < n; e += 64) {
-            const int j = e / NX, i = e - j * NX, k1 = 2 * j + 1;
-            const double* g1 = L.G + (size_t)k1 * NX * GS;
-            const double* p1 = L.dpv + (size_t)k1 * NX;
-            double acc = -fma(L.hq[k1 * NB + i], L.dxv[(size_t)k1 * NX + i], L.gq[k1 * NB + i]);
-#pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(g1[l * GS + i], p1[l], acc);
-            L.dpv[(size_t)(2 * j) * NX + i] = acc;
-        }
-        WSYNC();
-    }
-
-    // Step of stage kq from the condensed solution: dx (every stage expanded), du from K^ of its
-    // block, dpi (every stage expanded).
-    __device__ static void recover_cond(const Lds& L, int H, int kq, double (&dd)[NB], double (&dpi)[NX]) {
-        const int k = min(kq, H), j = min(k >> 1, (H >> 1) - 1), sl = (k & 1) * NU;
-        double x0[NX];
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            dd[i] = L.dxv[(size_t)k * NX + i];
-            x0[i] = L.dxv[(size_t)(2 * j) * NX + i];
-            dpi[i] = kq < H ? L.dpv[(size_t)k * NX + i] : 0.0;
-        }
-        const double* Kj = L.K + (size_t)j * NCU * PS + sl * PS;
-#pragma unroll
-        for (int a = 0; a < NU; ++a) {
-            double du = Kj[a * PS + NX];
-#pragma unroll
-            for (int c = 0; c < NX; ++c) du = fma(Kj[a * PS + c], x0[c], du);
-            dd[NX + a] = kq < H ? du : 0.0;
-        }
-    }
-
-    // Corrector with the condensed factorisation unchanged (mfma4_vector_backward over blocks):
-    //   p_j = vt_j + A^_j,x^T p_{j+1},  vt_j = q^_j + K^_j^T r^_j + A^_j,x^T t_j,  t_j = P_{j+1} c^_j,
-    //   kff^_j = -Ru_j^-1 (r^_j + G^_u^T (t_j + p_{j+1})),
-    // with [q^; r^] the block gradient (column CI of T^T D_x,k1 T + D^ at the current gq):
-    //   grad^[t] = sum_m T[m][t] (h_m c_k0[m] + g_m) + D^[t][CI].
-    // Scratch: q^ | r^ in dpv (rewritten by cond_expand after the sweep), t in Tc, vt in dxv.
-    __device__ static void cond_vector_backward(const Lds& L, int H, int lane) {
-        const int HB = H >> 1;
-        double* QH = L.dpv;                     // [HB][NX]
-        double* RH = L.dpv + (size_t)HB * NX;   // [HB][NCU]
-        constexpr int NT = NX + NCU;
-        // C1: block gradients (one (j, t) per lane) and t_j = P_{j+1} c^_j (one (j, i) per lane)
-        for (int e = lane; e < HB * (NT + NX); e += 64) {
-            if (e < HB * NT) {
-                const int j = e / NT, t = e - j * NT;   // t < NX: x_k0[t]; else input slot q = t - NX
-                const int k0 = 2 * j, k1 = k0 + 1;
-                const double* G0 = L.G + (size_t)k0 * NX * GS;
-                const int q = t - NX;
-                const bool tin = t < NX || q < NU;      // x_k0 or u_k0: a column of T
-                const int gcol = t < NX ? t : NX + (q < NU ? q : 0);
-                double acc = 0.0;
-#pragma unroll
-                for (int m = 0; m < NX; ++m) {
-                    const double w = fma(L.hq[k1 * NB + m], G0[m * GS + NB], L.gq[k1 * NB + m]);
-                    acc = fma(G0[m * GS + gcol], w, acc);
-                }
-                acc = tin ? acc : 0.0;
-                const int st = (t >= NX && q >= NU) ? k1 : k0;
-                const int v = t < NX ? t : NX + (q < NU ? q : q - NU);
-                acc += L.gq[st * NB + v];
-                if (t < NX) QH[(size_t)j * NX + t] = acc;
-                else RH[(size_t)j * NCU + q] = acc;
-            } else {
-                const int f = e - HB * NT, j = f / NX, i = f - j * NX;
-                const double* Pn = L.P + (size_t)(j + 1) * PP;
-                const double* gh = L.Gh + (size_t)j * NX * GH;
-                double acc = 0.0;
-#pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], gh[l * GH + NX], acc);
-                L.Tc[f] = acc;
-            }
-        }
-        WSYNC();
-        // C2: vt_j[i] = q^[i] + sum_q K^[q][i] (r^[q] + (G^_u^T t)[q]) + (G^_x^T t)[i]   (into dxv)
-        for (int e = lane; e < HB * NX; e += 64) {
-            const int j = e / NX, i = e - j * NX;
-            const double* gh = L.Gh + (size_t)j * NX * GH;
-            const double* Kj = L.K + (size_t)j * NCU * PS;
-            const double* tj = L.Tc + (size_t)j * NX;
-            double tv[NX];
-#pragma unroll
-            for (int l = 0; l < NX; ++l) tv[l] = tj[l];
-            double acc = QH[e];
-#pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(gh[l * GH + i], tv[l], acc);
-#pragma unroll
-            for (int q = 0; q < NCU; ++q) {
-                double bt = RH[(size_t)j * NCU + q];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) bt = fma(gh[l * GH + NX + 1 + q], tv[l], bt);
-                acc = fma(Kj[q * PS + i], bt, acc);
-            }
-            L.dxv[e] = acc;
-        }
-        WSYNC();
-        // C3: p_j = vt_j + A^_j,x^T p_{j+1}: [p_j; 1] = M_j [p_{j+1}; 1], M_j = [[A^_j,x^T, vt_j], [0, 1]],
-        // the entries of A^_j,x^T formed from G^_j and K^_j a block ahead
-        {
-            const Mfma4Lane q = mfma4_lane(lane);
-            const bool lda = q.row < NX && q.col < NX, ldv = q.row < NX && q.col == NX;
-            const bool one = q.row == NX && q.col == NX;
-            // A^[col][row]: row `col` of G^, column `row` of K^
-            const double* gr = L.Gh + ((size_t)(HB - 1) * NX + (lda ? q.col : 0)) * GH;
-            const double* kc = L.K + (size_t)(HB - 1) * NCU * PS + (lda ? q.row : 0);
-            const int gcol = lda ? q.row : 0;
-            const int gs = lda ? NX * GH : 0, ks = lda ? NCU * PS : 0;
-            const double* vp = L.dxv + (size_t)(HB - 1) * NX + (ldv ? q.row : 0);
-            const int vs = ldv ? NX : 0;
-            if (lane < NX) L.P[(size_t)HB * PP + PO + lane] = L.gq[H * NB + lane];
-            double y = mfma4_vec(q, [&](int i) { return L.gq[H * NB + i]; });
-            const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
-            const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
-            double* out = stlo ? L.P + (size_t)(HB - 1) * PP + PO + q.r
-                               : (sthi ? L.P + (size_t)(HB - 1) * PP + PO + 4 + q.r : L.dummy + lane);
-            const int ost = (stlo || sthi) ? PP : 0;
-            CondOp o0, o1;
-            double v0, v1;
-            cond_op_load(gr, kc, gcol, o0);
-            v0 = *vp;
-            auto step = [&](const CondOp& op, double vv) {
-                const double a = lda ? cond_op(op) : (ldv ? vv : (one ? 1.0 : 0.0));
-                double sv;
-                y = mfma4_stage(a, y, sv);
-                *out = sv;
-                out -= ost;
-            };
-            int j = HB - 1;
-            for (; j >= 1; j -= 2) {
-                gr -= gs; kc -= ks; vp -= vs;
-                cond_op_load(gr, kc, gcol, o1);
-                v1 = *vp;
-                step(o0, v0);
-                if (j >= 2) {
-                    gr -= gs; kc -= ks; vp -= vs;
-                    cond_op_load(gr, kc, gcol, o0);
-                    v0 = *vp;
-                }
-                step(o1, v1);
-            }
-            if (j == 0) step(o0, v0);
-        }
-        WSYNC();
-        // C4: kff^_j = -Ru_j^-1 (r^_j + G^_u^T (t_j + p_{j+1}))
-        for (int e = lane; e < HB * NCU; e += 64) {
-            const int j = e / NCU, a = e - j * NCU;
-            const double* gh = L.Gh + (size_t)j * NX * GH;
-            const double* pn = L.P + (size_t)(j + 1) * PP + PO;
-            double wv[NX];
-#pragma unroll
-            for (int l = 0; l < NX; ++l) wv[l] = L.Tc[(size_t)j * NX + l] + pn[l];
-            double kf = 0.0;
-#pragma unroll
-            for (int b2 = 0; b2 < NCU; ++b2) {
-                double acc = RH[(size_t)j * NCU + b2];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(gh[l * GH + NX + 1 + b2], wv[l], acc);
-                kf = fma(L.Rui[(size_t)j * NCU * NCU + a * NCU + b2], acc, kf);
-            }
-            L.K[(size_t)j * NCU * PS + a * PS + NX] = -kf;
-        }
-        WSYNC();
-    }
-
     // ------------------------------------------------------------------ Riccati on MFMA, NX <= 12, NU <= 4
     // For stages wider than one 16x16 tile (quad3d: NX = 12, NU = 4, NB + 1 = 17) the products are
     // split over two column tiles of v_mfma_f64_16x16x4_f64: T1 = [x | c] (c at tile column NX) and
@@ -2034,11 +1447,10 @@ struct SqpKernel {
     }
 
     // Step of stage kq from the Riccati solution, restricted to this lane's variables, and dpi_kq.
-    template <int NV, int CF>
+    template <int NV>
     __device__ static void recover_q(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
         double ddf[NB];
-        if constexpr (CF == 2) recover_cond(L, H, kq, ddf, dp);
-        else if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
+        if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
         else recover_step(L, H, kq, ddf, dp);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
@@ -2192,7 +1604,7 @@ struct SqpKernel {
     // One QP of the SQP iteration: blo/bup/gv/hd/d (this lane's variables) and cqq (the stage's
     // dynamics residual) in, the step d, the bound multipliers and piq (dynamics multipliers of
     // stage kq) out.  Every wave of the instance calls it (WSPL) with the same control flow.
-    template <bool SPL, int NV, int CF>
+    template <bool SPL, int NV>
     __device__ static bool qp_ipm(const ProblemDev& P, const Lds& L, int H, int lane, int wv,
                                   const double (&blo)[NV], const double (&bup)[NV], const double (&gv)[NV],
                                   const double (&hd)[NV], double (&d)[NV], const double (&cqq)[NX], double (&ll)[NV],
@@ -2226,10 +1638,6 @@ struct SqpKernel {
         }
 #pragma unroll
         for (int i = 0; i < NX; ++i) piq[i] = 0.0;
-        if constexpr (CF == 2) {   // G^_x, G^_u of this SQP iteration's linearisation
-            if (wv == 0) cond_ghat<true>(L, H, lane);
-            WSYNC();
-        }
         bool qp_ok = true;
         int qit = 0, par = 0;
         TPHASE(3);
@@ -2285,32 +1693,19 @@ struct SqpKernel {
                 if constexpr (kMfma) {
                     bool rok = true;
                     if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
-                        if constexpr (CF == 2) {
-                            cond_ghat<false>(L, H, lane);   // c^ of the current dynamics residual
-                            WSYNC();
-                            TPHASE(4);
-                            rok = cond_backward(L, H, lane);
-                            WSYNC();
-                            TPHASE(6);
-                            if (rok) cond_forward(L, H, lane);
-                            WSYNC();
-                            TPHASE(9);
-                            if (rok) cond_expand(L, H, lane);
-                        } else {
-                            rok = mfma_backward_h(L, H, lane);
-                            WSYNC();
-                            TPHASE(8);
-                            if (rok) acl_phase<true>(L, H, lane);
-                            WSYNC();
-                            TPHASE(6);
-                            if (rok) mfma4_forward(L, H, lane);
-                        }
+                        rok = mfma_backward_h(L, H, lane);
+                        WSYNC();
+                        TPHASE(8);
+                        if (rok) acl_phase<true>(L, H, lane);
+                        WSYNC();
+                        TPHASE(6);
+                        if (rok) mfma4_forward(L, H, lane);
                         WSYNC();
                     }
                     if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
-                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else {
                     // the recursion on wave 0 (WSPL: the other waves wait at the status exchange)
@@ -2325,7 +1720,7 @@ struct SqpKernel {
                     if constexpr (WSPL) rok = xall(L, lane, wv, par, rok);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(3);
-                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
                 }
                 // affine step: ds/s = q, dl/l = -1 - q (predictor r_m = l s); ratio test
                 // alpha_max = 1 / max(1, max_i -dv_i / v_i)
@@ -2372,26 +1767,17 @@ struct SqpKernel {
                 TPHASE(5);
                 if constexpr (kMfma) {
                     if (wv == 0) {
-                        if constexpr (CF == 2) {
-                            cond_vector_backward(L, H, lane);
-                            TPHASE(6);
-                            cond_forward(L, H, lane);
-                            WSYNC();
-                            TPHASE(9);
-                            cond_expand(L, H, lane);
-                        } else {
-                            mfma4_vector_backward(L, H, lane);
-                            TPHASE(8);
-                            acl_phase<false>(L, H, lane);
-                            WSYNC();
-                            TPHASE(6);
-                            mfma4_forward(L, H, lane);
-                        }
+                        mfma4_vector_backward(L, H, lane);
+                        TPHASE(8);
+                        acl_phase<false>(L, H, lane);
+                        WSYNC();
+                        TPHASE(6);
+                        mfma4_forward(L, H, lane);
                         WSYNC();
                     }
                     XSYNC();
                     TPHASE(9);
-                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
                 } else {
                     if (wv == 0) {
@@ -2401,7 +1787,7 @@ struct SqpKernel {
                     }
                     XSYNC();
                     TPHASE(3);
-                    recover_q<NV, CF>(L, H, kq, vb, dd, dp);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
                 }
                 rmax = 1.0;
                 double dsl[NV], dsu[NV], dll[NV], dlu[NV];
@@ -2457,7 +1843,6 @@ struct SqpKernel {
     // ends the loop with command -1 at the end of the kernel (one more B1).
     // Command -2 (WSPL): the wave takes its variables' share of the QP (qp_ipm) and publishes its
     // part of the step at B2.
-    template <int CF>
     __device__ static void helper_loop(const ProblemDev& P, const StateDev& S, const Lds& L, int w, int lane, int b) {
         const int H = P.H;
         const int ne = (H + 15) >> 4, np = 16 * ne;
@@ -2472,9 +1857,9 @@ struct SqpKernel {
                     qp_setup_pub<NV>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq);
                     Tm tm{};
                     int qit = 0;
-                    const bool ok = qp_ipm<false, NV, CF>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
+                    const bool ok = qp_ipm<false, NV>(P, L, H, lane, w, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
                     if (ok && lane <= H) {   // this wave's bound multipliers (acados memory)
-                        double* lam_q = lds_mult(CF) ? L.lam + (size_t)lane * 2 * NB
+                        double* lam_q = lds_mult ? L.lam + (size_t)lane * 2 * NB
                                                      : S.lam + ((size_t)b * (H + 1) + lane) * 2 * NB;
 #pragma unroll
                         for (int j = 0; j < NV; ++j) {
@@ -2503,17 +1888,16 @@ struct SqpKernel {
 
     // ------------------------------------------------------------------ the kernel body
     // SPL: the QP's per-variable state is split over two lanes per stage (needs H + 1 <= 32)
-    // CF: stages per block of the Newton-system recursions (2: condensed, needs kCond and H even)
-    template <bool SPL, int CF>
+    template <bool SPL>
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
         const int lane = threadIdx.x & 63;
         const int b = S.order ? __builtin_amdgcn_readfirstlane(S.order[blockIdx.x]) : (int)blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
-        const Lds L = carve<CF>(smem, H);
+        const Lds L = carve(smem, H);
         if constexpr (NWAVES > 1) {
             if (threadIdx.x >= 64) {   // GP helper wave
-                helper_loop<CF>(P, S, L, threadIdx.x >> 6, lane, b);
+                helper_loop(P, S, L, threadIdx.x >> 6, lane, b);
                 return;
             }
         }
@@ -2547,7 +1931,7 @@ struct SqpKernel {
         // this kernel): they live in LDS during the step (this lane's rows of L.lam / L.pim) and go
         // to global memory (S.lam / S.pi) once, at the end of the step, when the layout has room
         // (lds_mult); otherwise every SQP iteration reads and writes the global rows.
-        constexpr bool kLM = lds_mult(CF);
+        constexpr bool kLM = lds_mult;
         double w[NB];
         const double* xg = S.x + (size_t)b * (H + 1) * NX;
         const double* ug = S.u + (size_t)b * H * NU;
@@ -2817,7 +2201,7 @@ struct SqpKernel {
                 }
             }
             int qit = 0;
-            const bool qp_ok = qp_ipm<SPL, NV, CF>(P, L, H, lane, 0, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
+            const bool qp_ok = qp_ipm<SPL, NV>(P, L, H, lane, 0, blo, bup, gv, hd, d, cqq, ll, lu, piq, qit, tm);
             if constexpr (WSPL) qp_publish_step<NV>(L, H, lane, 0, d);   // B2: the full step in Dq
             qp_total += qit;
             TPHASE(2);
@@ -2983,16 +2367,16 @@ __global__ __launch_bounds__(256) void order_by_cost_kernel(const uint32_t* __re
 }
 
 // One wave per SIMD: every wave of an instance owns a SIMD's register file.
-template <int ID, int NW, bool SPL, int CF>
+template <int ID, int NW, bool SPL>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
-    SqpKernel<ID, NW>::template run<SPL, CF>(P, S, io);
+    SqpKernel<ID, NW>::template run<SPL>(P, S, io);
 }
 
-template <int ID, int NW, bool SPL, int CF>
+template <int ID, int NW, bool SPL>
 hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
-    const size_t lds = SqpKernel<ID, NW>::lds_doubles(P.H, CF) * sizeof(double);
+    const size_t lds = SqpKernel<ID, NW>::lds_doubles(P.H) * sizeof(double);
     if (lds > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL, CF>,
+        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
@@ -3010,17 +2394,8 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
     } else {
         Sl.order = nullptr;
     }
-    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, CF>), dim3(batch), dim3(64 * NW), lds, stream, P, Sl, io);
+    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL>), dim3(batch), dim3(64 * NW), lds, stream, P, Sl, io);
     return hipGetLastError();
-}
-
-template <int ID, int NW, bool SPL>
-hipError_t launch_sqp_cf(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
-    using K = SqpKernel<ID, NW>;
-    if constexpr (K::kCond) {
-        if (P.condense && K::cf_of(P.H) == 2) return launch_sqp_variant<ID, NW, SPL, 2>(P, S, io, batch, stream);
-    }
-    return launch_sqp_variant<ID, NW, SPL, 1>(P, S, io, batch, stream);
 }
 
 // waves per instance for this launch: the model's default, or (single-tile models) as many as the
@@ -3045,13 +2420,13 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
         const bool spl = P.H + 1 <= 32;
         const int nw = sqp_waves<ID>(P, batch);
         if (nw == 4)
-            return spl ? launch_sqp_cf<ID, 4, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 4, false>(P, S, io, batch, stream);
+            return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream);
         if (nw == 2)
-            return spl ? launch_sqp_cf<ID, 2, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 2, false>(P, S, io, batch, stream);
-        return spl ? launch_sqp_cf<ID, 1, true>(P, S, io, batch, stream) : launch_sqp_cf<ID, 1, false>(P, S, io, batch, stream);
+            return spl ? launch_sqp_variant<ID, 2, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 2, false>(P, S, io, batch, stream);
+        return spl ? launch_sqp_variant<ID, 1, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 1, false>(P, S, io, batch, stream);
     } else {
         // multi-wave models split the IPM state over their waves instead (WSPL)
-        return launch_sqp_cf<ID, kDefaultWaves<ID>, false>(P, S, io, batch, stream);
+        return launch_sqp_variant<ID, kDefaultWaves<ID>, false>(P, S, io, batch, stream);
     }
 }
 
@@ -3072,9 +2447,7 @@ int model_unc_dims(int model, int32_t* unc) {
 
 template <int ID>
 static size_t lds_bytes_of(int H) {   // the larger of the default-wave layouts a launch may pick
-    using K = SqpKernel<ID>;
-    const size_t a = K::lds_doubles(H, 1), b = K::lds_doubles(H, K::cf_of(H));
-    return (a > b ? a : b) * sizeof(double);
+    return SqpKernel<ID>::lds_doubles(H) * sizeof(double);
 }
 
 size_t sqp_lds_bytes(int model, int H) {

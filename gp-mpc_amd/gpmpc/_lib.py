@@ -43,7 +43,7 @@ SIGNATURES = {
     "gpmpc_gp_mean_grad": (_I, [_P, _I, _P, _I, _P, _P, _P]),
     "gpmpc_gp_posterior": (_I, [_I, _I, _I, _P, _P, _D, _D, _D, _P, _I, _P, _P, _I, _P]),
     "gpmpc_plant_step": (_I, [_P, _I, _P, _P, _P, _P, _P, _P]),
-    "gpmpc_set_launch": (_I, [_P, _I, _I]),
+    "gpmpc_set_launch": (_I, [_P, _I]),
     "gpmpc_set_profiling": (_I, [_P, _I]),
     "gpmpc_kernel_times": (_I, [_P, POINTER(_D), POINTER(_I), POINTER(_D), POINTER(_I)]),
     "gpmpc_kernel_time_list": (_I, [_P, _I, _P, _P, _P, _P]),

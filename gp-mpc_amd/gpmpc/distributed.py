@@ -158,12 +158,12 @@ def mll_and_grad_partial(gp, rows: slice | None = None):
     return mll, grad
 
 
-def fit_gp_allreduce(gp, n_train: int = 500, lr: float = 0.01) -> int:
+def fit_gp_allreduce(gp, n_train: int = 500, lr: float = 0.01, history: list | None = None) -> int:
     """Data-parallel Adam on −MLL (`gpmpc/gp.py:49-69`): each rank owns a contiguous row slice of
     the trace term, one all-reduce (sum) of the 3 gradient partials per iteration (RCCL over
     xGMI on the GPUs, gloo on CPU), every rank applies the same Adam step, so the replicas stay
     identical without a broadcast.  Early stop |Δloss| < 1e-3 like the reference.  Returns the
-    number of Adam iterations."""
+    number of Adam iterations; ``history`` as in :func:`gpmpc.gp.fit_gp`."""
     import math as _m
 
     rank, size = world()
@@ -190,6 +190,8 @@ def fit_gp_allreduce(gp, n_train: int = 500, lr: float = 0.01) -> int:
             p.grad = -gi.reshape(p.shape).clone()   # loss = -MLL
         opt.step()
         loss = -float(mll)
+        if history is not None:
+            history.append((loss, [float(p) for p in params]))
         if abs(last - loss) < 1e-3:
             break
         last = loss

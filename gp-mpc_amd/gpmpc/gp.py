@@ -224,8 +224,13 @@ def exact_mll(gp: GaussianProcess) -> torch.Tensor:
     return ll / n
 
 
-def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: str = "cpu") -> None:
-    """Adam on -MLL with early stopping |dloss| < 1e-3, then K, K_inv (`gpmpc/gp.py:49-69`)."""
+def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: str = "cpu",
+           history: list | None = None) -> int:
+    """Adam on -MLL with early stopping |dloss| < 1e-3, then K, K_inv (`gpmpc/gp.py:49-69`).
+
+    Returns the number of Adam steps taken.  ``history`` (optional list) receives one
+    ``(loss before the step, raw parameters after it)`` pair per step, for the parity tests
+    against the fit oracle (oracle/gp_fit_oracle.py)."""
     assert isinstance(gp, GaussianProcess), f"gp must be a GaussianProcess, got {type(gp)}"
     gp.to(device)
     params = gp.parameters()
@@ -233,12 +238,15 @@ def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: st
         p.requires_grad_(True)
     optim = torch.optim.Adam(params, lr=lr)
     last = math.inf
-    for _ in range(n_train):
+    it = 0
+    for it in range(1, n_train + 1):
         optim.zero_grad()
         loss = -exact_mll(gp)
         loss.backward()
         optim.step()
         lv = float(loss.detach())
+        if history is not None:
+            history.append((lv, [float(p.detach()) for p in params]))
         if abs(last - lv) < 1e-3:
             break
         last = lv
@@ -246,6 +254,7 @@ def fit_gp(gp: GaussianProcess, n_train: int = 500, lr: float = 0.01, device: st
         p.requires_grad_(False)
     gp._dev = None
     gp.K, gp.K_inv = gp.compute_covariances()
+    return it
 
 
 # gpytorch.settings.max_cholesky_size default: below it the LOVE cache is the exact Cholesky root

@@ -193,10 +193,10 @@ class BatchSolver:
         self._stats = buf
         _lib.check(self.lib.gpmpc_set_stats_buffer(self._h, None if buf is None else buf.data_ptr(), self.STATS_SLOTS))
 
-    def set_launch(self, waves: int = 0, condense: bool = False):
-        """SQP-kernel launch shape (gpmpc_set_launch): waves per instance (0 auto, 1, 2, 4) and the
-        condensed stage-pair recursions.  Performance options; results agree to rounding."""
-        _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves), int(bool(condense))))
+    def set_launch(self, waves: int = 0):
+        """SQP-kernel launch shape (gpmpc_set_launch): waves per instance (0 auto, 1, 2, 4; quad3d:
+        0 or 4).  A performance option; results agree to rounding."""
+        _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves)))
 
     def set_profiling(self, enabled: bool):
         _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))

@@ -9,6 +9,10 @@
  *
  * Threading: one handle per GPU/process, driven by one host thread at a time
  * (the reference drives one acados solver from one Python thread, gpmpc/gpmpc.py:105-107).
+ * Streams: every call queues its work on its stream argument.  The handle's device state is
+ * shared by all of them, so when a call names a different stream than the previous call, the
+ * handle first waits on the host for the previous stream's work; use one stream per handle
+ * (what BatchSolver does) to keep every call asynchronous.
  */
 #ifndef GPMPC_MI355X_H
 #define GPMPC_MI355X_H
@@ -139,7 +143,9 @@ gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, d
 
 /* Copy the GP variances the last tightening used (the variance kernel's output at the previous
  * solution, likelihood noise included, gpmpc/gpmpc.py:437-445) into var [B][H][n_gp] (device).
- * Diagnostic / parity surface: the values the constraint tightening consumed. */
+ * Diagnostic / parity surface: the values the constraint tightening consumed.  GPMPC_ERR_STATE
+ * when the last gpmpc_solve ran no variance launch (first step after a reset, tightening or GPs
+ * off): there are no such values; GPMPC_ERR_ARG when batch exceeds that launch's batch. */
 gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev, void* stream);
 
 /* GP posterior at P points Z [P][d] (device): mean [P] and/or variance [P] (either may be
@@ -173,11 +179,11 @@ gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* para
  *   waves     0 = auto: one wavefront per instance, or -- for the models whose stage fits one MFMA
  *             tile (quad2d, cartpole) -- four per instance when batch <= the device's compute units
  *             and two when batch <= twice that, so the SIMDs that would idle take the GP tile sums;
- *             1 / 2 / 4 force a count (quad3d always runs four).
- *   condense  1 = the Newton systems' Riccati recursions run over condensed stage pairs when H is
- *             even (single-tile models), 0 (default) = stage by stage.
- * Results are identical up to floating-point rounding; both are performance options. */
-gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves, int32_t condense);
+ *             1 / 2 / 4 force a count for quad2d / cartpole.  quad3d always runs four: it accepts
+ *             0 or 4 and rejects any other count (GPMPC_ERR_ARG), so a setting never silently
+ *             does nothing.
+ * Results are identical up to floating-point rounding; a performance option. */
+gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves);
 
 /* Kernel timing with HIP events recorded on the solve stream around the variance kernel
  * and the SQP kernel of every gpmpc_solve while enabled.  gpmpc_kernel_times synchronises

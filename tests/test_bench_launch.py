@@ -55,6 +55,23 @@ def test_global_batch_strong_scaling_slices():
         assert max(len(x) for x in sl) - min(len(x) for x in sl) <= 1
 
 
+def test_default_partition_is_the_metrics_global_batch():
+    """Without --batch, --gpus N splits the metric's global batch 1024 over the N ranks (strong
+    scaling: the driver's SCALE runs measure "batch 1024 @1/2/4/8 GPU"), and the line carries the
+    weak per-GPU figure (1024 instances on every GPU) as a secondary field."""
+    out = _run(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "0"])
+    assert out["scaling"] == "strong" and out["config"]["global_batch"] == 1024
+    assert out["config"]["batch_per_gpu"] == 512
+    assert [s[:2] for s in out["shards"]] == [[0, 512], [512, 1024]]
+    w = out["weak_per_gpu"]
+    assert w["scaling"] == "weak" and w["batch_per_gpu"] == 1024
+    assert [s[:2] for s in w["shards"]] == [[0, 1024], [1024, 2048]]
+    assert abs(w["value"] - 2048 * 3 / (w["ms_per_step"] * 3e-3)) <= 1e-6 * w["value"]
+    one = _run(["--gpus", "1", "--dry-run", "--steps", "2", "--warmup", "0"])
+    assert one["scaling"] == "strong" and one["config"]["global_batch"] == 1024 and one["weak_per_gpu"] is None
+    assert one["shards"][0][:2] == [0, 1024]
+
+
 def test_single_rank_needs_no_launcher():
     out = _run(["--gpus", "1", "--dry-run", "--batch", "4", "--steps", "2", "--warmup", "0"])
     assert out["n_gpus"] == 1 and out["shards"] == [[0, 4, out["shards"][0][2]]]

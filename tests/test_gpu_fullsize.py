@@ -57,6 +57,32 @@ def test_config3_full_batch_converges_at_default_tolerances():
         gs.plant_step(obs, u, ts, out=obs)
 
 
+def test_config2_full_batch_converges_at_default_tolerances():
+    """Config 2 (cartpole, N=50, H=20, B=256) at the bench defaults and the automatic launch shape
+    (four waves per instance: B <= CUs): every instance-step converges with all four NLP residuals
+    below 1e-6 over 12 closed-loop steps from a cold start."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem("cartpole", 50)
+    H, B, steps = 20, 256, 12
+    gs = BatchSolver(spec, H, B)
+    gs.set_gps(product_gps(data, hyp))
+    gs.set_tightening(True, 0.95, *lqr(spec))
+    gs.reset(reset_iterate=True)
+    x0, ph = initial_states(spec, spec.reference_trajectory(), B, seed=1)
+    obs = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    for k in range(steps):
+        u = gs.solve(obs, ts)
+        st = gs.status.cpu().numpy()
+        res = gs.res.cpu().numpy()
+        assert (st == 0).all(), (k, np.bincount(st, minlength=5))
+        assert res.max() <= 1e-6, (k, res.max(axis=0))
+        assert torch.isfinite(u).all()
+        gs.plant_step(obs, u, ts, out=obs)
+
+
 def test_config4_full_batch_converges_with_love_variance():
     """Config 4 per GPU (quad2d, N=1000, H=30, B=1024) at the bench defaults: the tightening
     variance from the LOVE roots (gpytorch fast_pred_var above 800 rows, `gpmpc/gpmpc.py:441-445`);

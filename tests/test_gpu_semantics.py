@@ -213,3 +213,34 @@ def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
         if model == "quad2d":
             assert (outs[0][1] == 0).all(), outs[0][1]
         x = on.plant_step(x, outs[0][0])
+
+
+def test_variance_readback_only_after_a_variance_launch():
+    """gpmpc_get_variance returns what the last tightening used, or refuses: after a reset (first
+    step, no previous solution) the solve runs no variance launch and there is nothing to return;
+    after the next step it returns the launch's values (likelihood noise included, so > 0)."""
+    torch = _torch()
+    from gpmpc import _lib
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem("quad2d", 40)
+    H, B = 10, 3
+    gs = BatchSolver(spec, H, B)
+    gs.set_gps(product_gps(data, hyp))
+    gs.set_tightening(True, 0.95, *lqr(spec))
+    gs.reset(reset_iterate=True)
+    x0, ph = initial_states(spec, spec.reference_trajectory(), B)
+    obs = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    with pytest.raises(_lib.GPMPCError):
+        gs.variance()                       # nothing solved yet
+    u = gs.solve(obs, ts)                   # first step: no previous solution, no variance launch
+    with pytest.raises(_lib.GPMPCError):
+        gs.variance()
+    gs.plant_step(obs, u, ts, out=obs)
+    gs.solve(obs, ts)                       # variance launch at the previous solution
+    v = gs.variance().cpu().numpy()
+    assert v.shape == (B, H, spec.n_gp) and (v > 0).all()
+    gs.reset(reset_iterate=False)
+    with pytest.raises(_lib.GPMPCError):
+        gs.variance()

@@ -37,7 +37,6 @@ def main():
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference")
     ap.add_argument("--dump", default="", help="save the per-step per-instance phase cycles (.npy)")
     ap.add_argument("--waves", type=int, default=0, help="waves per instance (gpmpc_set_launch; 0 = auto)")
-    ap.add_argument("--condense", action="store_true", help="condensed stage-pair Riccati recursions")
     args = ap.parse_args()
     from gpmpc import _lib
     from gpmpc.gp import GaussianProcess
@@ -58,7 +57,7 @@ def main():
     dfdx, dfdu = spec.prior_jacobian(np.zeros(spec.nx), spec.u_eq)
     mats = setup_prior_dynamics(dfdx, dfdu, np.diag(spec.q_diag), np.diag(spec.r_diag), spec.dt)
     s = BatchSolver(spec, H, B)
-    s.set_launch(waves=args.waves, condense=args.condense)
+    s.set_launch(waves=args.waves)
     if args.no_gp:
         s.set_gps(None)
     else:
@@ -103,7 +102,7 @@ def main():
     sub = cyc[-1]            # GP sums: a sub-phase of "linearize", not part of the total
     cyc = cyc[:-1]
     ms = kt["sqp_ms"] / max(kt["sqp_launches"], 1)
-    print(f"waves {args.waves or 'auto'}, condense {args.condense}")
+    print(f"waves {args.waves or 'auto'}")
     print(f"{spec.name} B={B} H={H} N={N}: sqp kernel {ms:.3f} ms/launch, sqp_iter {s.sqp_iter.float().mean():.2f}, "
           f"qp_iter {s.qp_iter.float().mean():.2f}")
     print(f"cycles per instance (mean) {cyc.sum():.0f} -> {cyc.sum() / (ms * 1e-3) / 1e9:.2f} G cycles/s effective")
