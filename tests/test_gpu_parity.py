@@ -280,7 +280,12 @@ def test_closed_loop_parity_vs_cpp_restatement(name, N, H, B, steps, var):
         # residual sits at the 1e-11 QP tolerance)
         np.testing.assert_array_equal(gs.sqp_iter.cpu().numpy(), ref.sqp_iter)
         ok = st == 0   # instances that reach the 1e-9 KKT tolerance (both sides agree on which)
-        assert ok.mean() >= 0.75, (s, st)
+        # every instance-step converges except quad2d's one instance at step 1 that needs more than
+        # 25 SQP iterations at this tolerance (tools/status_census.py, profiles/r4/status_census.jsonl)
+        if name == "quad2d" and s == 1:
+            assert (~ok).sum() <= 1, (s, st)
+        else:
+            assert ok.all(), (s, st)
         err = np.abs(xg - ref.x).max(axis=(1, 2)) / (1 + np.abs(ref.x).max(axis=(1, 2)))
         assert err[ok].max() <= 1e-6, (s, err[ok].max())
         # instances stopped at the SQP iteration limit (status 2, both sides) ran the same iterations
