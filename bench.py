@@ -92,7 +92,7 @@ def cpu_threads() -> int:
 
 
 def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, x0_all, phase_all, ids, warmup, steps, fitc=None,
-                 love_roots=None):
+                 love_roots=None, qp_tol=None):
     """Time the C++ CPU restatement (oracle/cpu_ref.cpp: SQP-GN + Mehrotra IPM with Riccati
     Newton steps, OpenMP over instances, the same tightening variance as the GPU leg: exact or
     the same LOVE roots) on the GPU leg's own window: the same global instance ids (an evenly
@@ -111,7 +111,8 @@ def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, x0_all, phase_all, ids, 
     window = warmup + steps
 
     def run(sel, nthreads):
-        ref = cpu_ref.CpuRef(spec, H, len(sel), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots)
+        ref = cpu_ref.CpuRef(spec, H, len(sel), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots,
+                             qp_tol=qp_tol)
         x0 = x0_all[sel].copy()
         phase = phase_all[sel].astype(np.int32)
         elapsed, sqp = 0.0, 0
@@ -129,7 +130,8 @@ def cpu_baseline(spec, data, hyp, H, seconds, lqr_mats, x0_all, phase_all, ids, 
     # per-instance-step cost from one cold step of `threads` instances (an upper bound: the cold
     # step needs the most SQP iterations), then the largest sample the budget allows
     probe = ids[np.linspace(0, len(ids) - 1, min(threads, len(ids))).astype(int)]
-    ref = cpu_ref.CpuRef(spec, H, len(probe), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots)
+    ref = cpu_ref.CpuRef(spec, H, len(probe), gps=gps, lqr_mats=lqr_mats, fitc=fitc, love_roots=love_roots,
+                         qp_tol=qp_tol)
     t0 = time.perf_counter()
     ref.step(x0_all[probe].copy(), phase_all[probe].astype(np.int32), threads=threads)
     t_inst = (time.perf_counter() - t0) * threads / len(probe)     # core-seconds per instance-step
@@ -170,7 +172,9 @@ def parse_args(argv=None):
     ap.add_argument("--horizon", type=int, default=30)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--qp-tol", type=float, default=1e-8, help="IPM tolerance of the QP sub-problems")
+    ap.add_argument("--qp-tol", type=float, default=None,
+                    help="IPM tolerance of the QP sub-problems (default: the NLP tolerance 1e-6, as acados passes its "
+                         "NLP tolerances on to the QP solver)")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
@@ -427,7 +431,7 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         cpu = None
         if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
             cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, m["x0_all"], m["phase_all"], list(ids),
-                               args.warmup, args.steps, fitc=fitc, love_roots=solver.love_roots)
+                               args.warmup, args.steps, fitc=fitc, love_roots=solver.love_roots, qp_tol=args.qp_tol)
         sq = np.array(sqp_list) if sqp_list else np.zeros(1)
         out = {
             "metric": METRIC,

@@ -229,7 +229,10 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.max_iter = 25;          // gpmpc.py:262
     P.tol_stat = P.tol_eq = P.tol_ineq = P.tol_comp = 1e-6;  // acados defaults
     P.qp_max_iter = 50;   // acados qp_solver_iter_max default
-    P.qp_tol = 1e-8;     // HPIPM default residual tolerances (acados leaves qp_tol unset, gpmpc.py:257-263)
+    // QP tolerances = the NLP tolerances: gpmpc.py:257-263 leaves qp_solver_tol_* unset, and acados'
+    // SQP passes each NLP tolerance it is given (tol_stat/eq/ineq/comp, 1e-6 by default) on to the QP
+    // solver as that solver's tolerance (ocp_nlp_sqp_opts_set -> qp_solver opts_set "tol_stat", ...)
+    P.qp_tol = 1e-6;
     P.qp_mu0 = 1.0;
     P.lin_gen = 1;   // tags start at 0: nothing cached
     {

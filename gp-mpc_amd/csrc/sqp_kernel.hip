@@ -28,18 +28,6 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
-// Riccati factorisation of the single-tile models: M' and the Schur product on the 4-block MFMA
-// (1, default) or on v_mfma_f64_16x16x4 like W' (0: the round-3 form, for A/B)
-#ifndef GPMPC_RIC_HYBRID
-#define GPMPC_RIC_HYBRID 1
-#endif
-// Single-tile models on two or four waves per instance: the helper waves form the closed-loop maps
-// A'_k stage by stage behind the factorisation and the corrector's t_k = P_{k+1} c_k during the
-// predictor's forward sweep (1, default), or take GP tile passes only (0, for A/B)
-#ifndef GPMPC_HELPER_OVERLAP
-#define GPMPC_HELPER_OVERLAP 1
-#endif
-
 namespace gpmpc {
 
 // Orders the LDS traffic of the (main) wave.  One wave per block: __syncthreads.  With GP helper
@@ -323,10 +311,6 @@ struct SqpKernel {
     // main wave runs the recursions.  The single-tile models use the same protocol when the batch
     // is small enough for every instance to have a CU (B <= CUs): the idle SIMDs then do that work.
     static constexpr int NWAVES = NW;
-    // helper waves of the single-tile models overlap parts of every IPM iteration with wave 0's
-    // recursions (command kCmdOverlap of helper_loop)
-    static constexpr bool kOverlap = NW > 1 && kMfma && GPMPC_HELPER_OVERLAP != 0;
-    static constexpr int kCmdOverlap = -3;
     static_assert(NW == 1 || NW == 4 || (NW == 2 && kMfma), "one wave per instance, two (single-tile models) or four: one per SIMD");
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
@@ -790,25 +774,6 @@ struct SqpKernel {
     // The u rows sit at 8..8+NU-1 = lane groups 0..NU-1 of element 2: the Schur A operand needs no
     // lane move.  Stores of stage k are issued after stage k-1's W' products (sched_barrier), off
     // the chain.  Outputs: packed P', K' = [K | kff], Ru^-1 per stage.
-    //
-    // HY (hybrid): M' and the Schur product on v_mfma_f64_4x4x4_4b_f64 instead.  Read through that
-    // instruction's operand map (lane 16R + 4b + c: block b takes A_b[m][k] from lane (k, b, m),
-    // B_b[k][n] from (k, b, n), writes D_b[m][n] to (m, b, n)), register r of a 16x16 C-layout tile
-    // is block row r of the tile with block column b in slot b.  So
-    //   M'(I, J) = sum_K G''(K, I)^T W'(K, J) + D(I, J)     slot J: B = W' register K as it stands,
-    //                                                       A = block (K, I) of G'' replicated over
-    //                                                       the slots (its own LDS stream),
-    //                                                       C = the D register I as it stands
-    //   P'(I, J) = M'(I, J) + M'_u(., I)^T K'(., J)          slot J: A = block I of the u rows, moved
-    //                                                       to slot J by one bank-masked DPP row
-    //                                                       rotation (off the chain: beside K'),
-    //                                                       B = K' as it stands, C = M' register I
-    // (6 + 2 four-pass instructions for 2 + 1 sixteen-pass ones), and the outputs are again the C
-    // layout, so P' stays the next stage's 16x16 A operand and every store is unchanged.
-    // PROG: after the stores of stage k, publish k in L.ctrl[2] (the helpers' progress counter,
-    // kOverlap): LDS operations of a wave execute in issue order, and the stores and the counter
-    // write sit in one scheduling region, after the stores.
-    template <bool HY = GPMPC_RIC_HYBRID != 0, bool PROG = false>
     __device__ static bool mfma_backward_h(const Lds& L, int H, int lane) {
         const int lr = lane >> 4, lc = lane & 15;
         constexpr int CI = NX, UI = 8;
@@ -864,29 +829,7 @@ struct SqpKernel {
             pd[r] = on ? base + (size_t)(H - 1) * NB : L.zero;
             dst[r] = on ? NB : 0;
         }
-        // HY: G'' block (K, I) replicated over the slots: lane (R, b, c) <- G''[4K + R][4I + c]
-        constexpr int NXB = HY ? 6 : 1;
-        const double* px[NXB];
-        int pxst[NXB];
-#pragma unroll
-        for (int q = 0; q < NXB; ++q) {
-            const int K = q / 3, I = q % 3, c = lc & 3;
-            const int t = 4 * K + lr, gc_t = gcol(4 * I + c);
-            const bool ld = t < NX && gc_t >= 0;
-            const bool one = t == CI && 4 * I + c == CI;
-            px[q] = ld ? L.G + (size_t)(H - 1) * NX * GS + t * GS + gc_t : L.zero + (one ? 7 : 0);
-            pxst[q] = ld ? NX * GS : 0;
-        }
         struct Stage { double g[2], d[3]; };
-        // (HY: the replicated G'' blocks are read at the top of their own stage -- the W' products
-        // they wait behind take longer than the LDS reads -- so they need no second buffer)
-        auto load_x = [&](double (&x)[NXB]) {
-#pragma unroll
-            for (int q = 0; q < NXB; ++q) {
-                x[q] = *px[q];
-                px[q] -= pxst[q];
-            }
-        };
         auto load_stage = [&](Stage& st) {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
@@ -918,7 +861,6 @@ struct SqpKernel {
         const int srui_st = rst ? NU * NU : 0;
         double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
         bool pend = false;
-        int kpub = H - 1;   // PROG: the stage whose outputs the next flush stores
         auto flush = [&]() {
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
@@ -929,11 +871,6 @@ struct SqpKernel {
             sk -= sk_st;
             *srui = pend_r;
             srui -= srui_st;
-            if constexpr (PROG) {
-                __builtin_amdgcn_sched_barrier(0);
-                *(volatile int*)(L.ctrl + 2) = kpub;
-                --kpub;
-            }
         };
         auto flush_at = [&]() {   // the previous stage's stores, pinned after the W' products
             __builtin_amdgcn_sched_barrier(0);
@@ -942,25 +879,11 @@ struct SqpKernel {
             pend = true;
         };
         auto stage = [&](const Stage& sd) {
-            double x[NXB];
-            if constexpr (HY) load_x(x);
             f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
             w = mfma64(pn[1], sd.g[1], w);
             flush_at();
-            f64x4 m;
-            if constexpr (HY) {
-                // u rows first: Ru and M'_u gate the rest of the stage
-                m[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[2], w[0], sd.d[2], 0, 0, 0);
-                m[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[0], w[0], sd.d[0], 0, 0, 0);
-                m[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[1], w[0], sd.d[1], 0, 0, 0);
-                m[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[5], w[1], m[2], 0, 0, 0);
-                m[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[3], w[1], m[0], 0, 0, 0);
-                m[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(x[4], w[1], m[1], 0, 0, 0);
-                m[3] = 0.0;
-            } else {
-                m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
-                m = mfma64(sd.g[1], w[1], m);
-            }
+            f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
+            m = mfma64(sd.g[1], w[1], m);
             double Ru[NU][NU];
 #pragma unroll
             for (int a = 0; a < NU; ++a)
@@ -992,16 +915,7 @@ struct SqpKernel {
                 Ri[1][1] = Ru[0][0] * id;
                 Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
             }
-            f64x4 pk;
-            if constexpr (HY) {
-                // block I of the u rows in every slot J (slot I holds it: one bank-masked rotation)
-                const double x0 = dpp_merge<0x124, 0x2>(mu, mu);   // slot 1 <- slot 0 (row_ror:4)
-                const double x1 = dpp_merge<0x12C, 0x1>(mu, mu);   // slot 0 <- slot 1 (row_ror:12)
-                pk[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(x0, kb, m[0], 0, 0, 0);
-                pk[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(x1, kb, m[1], 0, 0, 0);
-            } else {
-                pk = mfma64(lr < NU ? mu : 0.0, kb, m);   // P'_k = M' + M'_{.u} K'
-            }
+            const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);   // P'_k = M' + M'_{.u} K'
             double rv = Ri[0][0];
             if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
             pend_p[0] = pk[0];
@@ -1202,29 +1116,6 @@ struct SqpKernel {
         }
     }
 
-    // Closed-loop map A'_k of one stage, entry (i, j) per lane (the arithmetic of acl_phase<true>,
-    // bit for bit): the helper waves' share of kOverlap, one stage at a time behind the factorisation.
-    __device__ static void acl_stage(const Lds& L, int k, int lane) {
-        if (lane >= NX * PS) return;
-        const int i = lane / PS, j = lane - i * PS;
-        const double* G = L.G + (size_t)k * NX * GS + i * GS;
-        const double* Kk = L.K + (size_t)k * NU * PS;
-        double acc = (j < NX) ? G[j] : G[NB];
-#pragma unroll
-        for (int a = 0; a < NU; ++a) acc = fma(G[NX + a], Kk[a * PS + j], acc);
-        L.Acl[(size_t)k * NX * PS + i * PS + j] = acc;
-    }
-    // t_k = P_{k+1} c_k, entry e = (k, i) (the corrector's first phase, mfma4_vector_backward)
-    __device__ static double t_entry(const Lds& L, int e) {
-        const int k = e / NX, i = e - k * NX;
-        const double* Pn = L.P + (size_t)(k + 1) * PP;
-        const double* G = L.G + (size_t)k * NX * GS;
-        double acc = 0.0;
-#pragma unroll
-        for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
-        return acc;
-    }
-
     // Closed-loop stage maps A'_k = [A + B K | B kff + c] (all stages in parallel); only the
     // affine column when the factorisation is unchanged (corrector).
     template <bool full>
@@ -1352,24 +1243,29 @@ struct SqpKernel {
     // with [q; r] = gq.  Only the p recurrence is sequential (one v_mfma_f64_4x4x4_4b + DPP merge per
     // stage, mfma4_stage); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
-    // SKIP_T: t_k is already in T (the helper waves formed it, kOverlap).
-    template <bool SKIP_T = false>
     __device__ static void mfma4_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
         // entries (k, i) two per pass, both computed before either is stored (T and VT alias other
         // LDS buffers, so a store would otherwise order the next entry's reads behind it)
         const int n = H * NX;
-        if constexpr (!SKIP_T) {
-            for (int e0 = lane; e0 < n; e0 += 128) {
-                const int e1 = e0 + 64;
-                const bool has1 = e1 < n;
-                const double a0 = t_entry(L, e0), a1 = t_entry(L, has1 ? e1 : e0);
-                T[e0] = a0;
-                if (has1) T[e1] = a1;
-            }
-            WSYNC();
+        auto t_entry = [&](int e) {
+            const int k = e / NX, i = e - k * NX;
+            const double* Pn = L.P + (size_t)(k + 1) * PP;
+            const double* G = L.G + (size_t)k * NX * GS;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
+            return acc;
+        };
+        for (int e0 = lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            T[e0] = a0;
+            if (has1) T[e1] = a1;
         }
+        WSYNC();
         auto vt_entry = [&](int e) {
             const int k = e / NX, i = e - k * NX;
             const double* A = L.Acl + (size_t)k * NX * PS;
@@ -1796,20 +1692,7 @@ struct SqpKernel {
                 double dd[NV], dp[NX];
                 if constexpr (kMfma) {
                     bool rok = true;
-                    if constexpr (kOverlap) {
-                        // helpers: A'_k behind the factorisation (progress counter), then t_k
-                        if (lane == 0) {
-                            L.ctrl[0] = kCmdOverlap;
-                            L.ctrl[2] = H;
-                        }
-                        __syncthreads();   // B1
-                        rok = mfma_backward_h<GPMPC_RIC_HYBRID != 0, true>(L, H, lane);
-                        __syncthreads();   // Bx: every A'_k written
-                        TPHASE(6);
-                        if (rok) mfma4_forward(L, H, lane);
-                        WSYNC();
-                        if (!rok) __syncthreads();   // B2 (the helpers' t_k), before leaving the QP
-                    } else if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
+                    if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
                         rok = mfma_backward_h(L, H, lane);
                         WSYNC();
                         TPHASE(8);
@@ -1883,16 +1766,7 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(5);
                 if constexpr (kMfma) {
-                    if constexpr (kOverlap) {
-                        __syncthreads();   // B2: t_k of every stage written by the helpers
-                        mfma4_vector_backward<true>(L, H, lane);
-                        TPHASE(8);
-                        acl_phase<false>(L, H, lane);
-                        WSYNC();
-                        TPHASE(6);
-                        mfma4_forward(L, H, lane);
-                        WSYNC();
-                    } else if (wv == 0) {
+                    if (wv == 0) {
                         mfma4_vector_backward(L, H, lane);
                         TPHASE(8);
                         acl_phase<false>(L, H, lane);
@@ -1976,26 +1850,6 @@ struct SqpKernel {
             __syncthreads();   // B1
             const int G = L.ctrl[0];
             if (G == -1) break;
-            if constexpr (kOverlap) {
-                if (G == kCmdOverlap) {
-                    // A'_k of stages H - w, H - w - (NW - 1), ... as soon as the factorisation has
-                    // stored their K'_k (wave 0 publishes k after the stores of stage k)
-                    for (int k = H - w; k >= 0; k -= NWAVES - 1) {
-                        // (bounded: a wave that never sees the counter move still reaches the barriers)
-                        for (int spin = 0; spin < (1 << 24) &&
-                                           __hip_atomic_load((int*)(L.ctrl + 2), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > k;
-                             ++spin)
-                            __builtin_amdgcn_s_sleep(1);
-                        acl_stage(L, k, lane);
-                    }
-                    __syncthreads();   // Bx
-                    // t_k = P_{k+1} c_k while wave 0 runs the predictor's forward sweep (T aliases hq,
-                    // dead until the corrector)
-                    for (int e = (w - 1) * 64 + lane; e < H * NX; e += (NWAVES - 1) * 64) L.hq[e] = t_entry(L, e);
-                    __syncthreads();   // B2
-                    continue;
-                }
-            }
             if constexpr (WSPL) {
                 if (G == -2) {
                     constexpr int NV = nv_of<false>();

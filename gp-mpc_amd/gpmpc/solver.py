@@ -57,7 +57,7 @@ class BatchSolver:
 
     def __init__(self, spec: ModelSpec, horizon: int, batch: int, device="cuda", prior_params: dict | None = None,
                  traj: np.ndarray | None = None, uh: float = -1e-8, cost_scaling: bool = True, max_iter: int = 25,
-                 tol: float = 1e-6, qp_max_iter: int = 50, qp_tol: float = 1e-8, qp_mu0: float = 1.0):
+                 tol: float = 1e-6, qp_max_iter: int = 50, qp_tol: float | None = None, qp_mu0: float = 1.0):
         self.lib = _lib.load()
         self.spec = spec
         self.H = int(horizon)
@@ -104,7 +104,11 @@ class BatchSolver:
             _c(spec.u_lo).ctypes.data, _c(spec.u_hi).ctypes.data, _c(spec.q_diag).ctypes.data,
             _c(spec.r_diag).ctypes.data, _c(spec.u_eq).ctypes.data, self._uh, self._cost_scaling))
 
-    def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=50, qp_tol=1e-8, qp_mu0=1.0):
+    def set_options(self, max_iter=25, tol=1e-6, qp_max_iter=50, qp_tol=None, qp_mu0=1.0):
+        """SQP / QP options (gpmpc_set_options).  ``qp_tol=None``: the QP solves to the NLP tolerance,
+        as acados passes its NLP tolerances on to the QP solver when the OCP leaves the QP
+        tolerances unset (`gpmpc/gpmpc.py:257-263`)."""
+        qp_tol = tol if qp_tol is None else qp_tol
         _lib.check(self.lib.gpmpc_set_options(self._h, int(max_iter), tol, tol, tol, tol, int(qp_max_iter), qp_tol, qp_mu0))
 
     def set_reference(self, traj: np.ndarray):

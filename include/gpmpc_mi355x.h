@@ -71,7 +71,9 @@ gpmpc_status gpmpc_set_model(gpmpc_handle* h, const double* params, int32_t n_pa
 gpmpc_status gpmpc_set_reference(gpmpc_handle* h, const double* traj_nx_by_L, int32_t L);
 
 /* SQP / QP options.  Reference: nlp_solver_max_iter = 25 (gpmpc/gpmpc.py:262); acados
- * default NLP tolerances 1e-6.  The QP options belong to the batched IPM. */
+ * default NLP tolerances 1e-6.  The QP options belong to the batched IPM: qp_max_iter 50
+ * (acados qp_solver_iter_max), qp_tol 1e-6 by default -- the OCP leaves the QP tolerances unset,
+ * and acados' SQP then passes its NLP tolerances on to the QP solver. */
 gpmpc_status gpmpc_set_options(gpmpc_handle* h, int32_t max_iter, double tol_stat, double tol_eq,
                                double tol_ineq, double tol_comp, int32_t qp_max_iter, double qp_tol, double qp_mu0);
 

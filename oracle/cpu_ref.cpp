@@ -106,7 +106,7 @@ struct Problem {
     double xlo[MX], xhi[MX], ulo[MU], uhi[MU], q[MX], r[MU], ueq[MU];
     bool cost_scaling = true, use_gp = false;
     int max_iter = 25, qp_max_iter = 50;
-    double tol = 1e-6, qp_tol = 1e-8;
+    double tol = 1e-6, qp_tol = 1e-6;   // acados: the QP solves to the NLP tolerances
     GP gp[MG];
     std::vector<double> traj;   // [L][nx]
     int traj_len = 0;

@@ -50,7 +50,7 @@ class CpuRef:
     """B instances of the control step on the host (GPMPC.select_action semantics, batched)."""
 
     def __init__(self, spec, H: int, B: int, gps=None, lqr_mats=None, prob: float = 0.95, uh: float = -1e-8,
-                 tol: float = 1e-6, qp_tol: float = 1e-8, qp_max_iter: int = 50, max_iter: int = 25, fitc=None,
+                 tol: float = 1e-6, qp_tol: float | None = None, qp_max_iter: int = 50, max_iter: int = 25, fitc=None,
                  love_roots=None):
         """``fitc[g] = (S (M, d), w (M,))``: GP g's mean over the inducing rows S with weights w
         (`gpmpc/gpmpc.py:175-187,377-400`); its variance stays the exact GP's (``gps[g]``).
@@ -69,7 +69,8 @@ class CpuRef:
                                         k[6].ctypes.data, k[7].ctypes.data, uh, 1)
         if not self.h:
             raise RuntimeError("cpuref_create failed")
-        self.lib.cpuref_set_options(self.h, max_iter, tol, qp_max_iter, qp_tol)
+        # qp_tol None: the NLP tolerance (acados passes its NLP tolerances on to the QP solver)
+        self.lib.cpuref_set_options(self.h, max_iter, tol, qp_max_iter, tol if qp_tol is None else qp_tol)
         traj = _c(spec.reference_trajectory().T)
         self._keep.append(traj)
         self.lib.cpuref_set_reference(self.h, traj.ctypes.data, traj.shape[0])
