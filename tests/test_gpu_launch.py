@@ -26,7 +26,7 @@ def _torch():
 def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True):
     """all_converge: every instance-step reaches KKT 1e-9 (tools/status_census.py, profiles/r4/
     status_census.jsonl); otherwise the ones stopped at the SQP iteration limit (status 2 on both
-    sides, at most 5 %) ran the same iterations from the same start and agree to 1e-4."""
+    sides, at most one instance or 5 %) ran the same iterations from the same start and agree to 1e-4."""
     torch = _torch()
     from oracle import cpu_ref
     from gpmpc.solver import BatchSolver
@@ -56,7 +56,7 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True):
         if all_converge:
             assert ok.all(), (s, np.bincount(st, minlength=5))   # every instance reaches KKT 1e-9
         else:
-            assert ok.mean() >= 0.95 and (st[~ok] == 2).all(), (s, np.bincount(st, minlength=5))
+            assert (~ok).sum() <= max(1, B // 20) and (st[~ok] == 2).all(), (s, np.bincount(st, minlength=5))
         err = np.abs(xg - ref.x).max(axis=(1, 2)) / (1 + np.abs(ref.x).max(axis=(1, 2)))
         assert err[ok].max() <= 1e-6, (s, err[ok].max())
         eu = np.abs(ug - ref.u).max(axis=(1, 2)) / (1 + np.abs(ref.u).max(axis=(1, 2)))

@@ -1,8 +1,9 @@
-// Micro-benchmark of the Riccati factorisation of SqpKernel<quad2d> / <cartpole> in isolation
-// (diagnostic only): the production device function mfma_backward_h in its two forms -- M' and the
-// Schur product on v_mfma_f64_16x16x4 (HY = false) or v_mfma_f64_4x4x4_4b (HY = true) -- on
-// synthetic stage data in LDS, one wave per instance, 1024 instances, plus an agreement check of
-// every output (packed P', K', Ru^-1) between the two forms.
+// Micro-benchmark of the Newton-system recursions of SqpKernel<quad2d> / <cartpole> in isolation
+// (diagnostic only): the production device functions mfma_backward_h (factorisation),
+// mfma4_forward (forward sweep) and mfma4_vector_backward (corrector) on synthetic stage data in
+// LDS, one wave per instance, 1024 instances; the sweeps with their stage operands one (PF = 1) or
+// two (PF = 2) stages ahead, and an agreement check between the two.
+// (The round-4 hybrid factorisation it also timed lives in tools/hybrid_riccati_overlap.patch.)
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 \
 //        -I gp-mpc_amd/csrc -o tools/ric_micro tools/ric_micro.hip
 #include <hip/hip_runtime.h>
@@ -30,9 +31,14 @@ __device__ void init_stage_data(const typename SqpKernel<ID>::Lds& L, int H, int
         L.gq[e] = 0.01 * ((e * (13 + salt)) % 7) - 0.03;
     }
     __syncthreads();
+    K::mfma_backward_h(L, H, lane);
+    __syncthreads();
+    K::template acl_phase<true>(L, H, lane);
+    __syncthreads();
 }
 
-template <int ID, bool HY>
+// V: 0 factorisation, 1 forward PF1, 2 forward PF2, 3 corrector PF1, 4 corrector PF2
+template <int ID, int V>
 __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long* out, double* sink) {
     using K = SqpKernel<ID>;
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -42,54 +48,67 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     bool ok = true;
     for (int r = 0; r < reps; ++r) {
-        ok = K::template mfma_backward_h<HY>(L, H, lane) && ok;
+        if constexpr (V == 0) ok = K::mfma_backward_h(L, H, lane) && ok;
+        if constexpr (V == 1) K::template mfma4_forward<1>(L, H, lane);
+        if constexpr (V == 2) K::template mfma4_forward<2>(L, H, lane);
+        if constexpr (V == 3) K::template mfma4_vector_backward<1>(L, H, lane);
+        if constexpr (V == 4) K::template mfma4_vector_backward<2>(L, H, lane);
         __syncthreads();
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) out[blockIdx.x] = t1 - t0;
-    if (lane < K::NX) sink[blockIdx.x * 8 + lane] = L.P[lane] + L.K[lane] + (ok ? 0.0 : 1.0);
+    if (lane < K::NX) sink[blockIdx.x * 8 + lane] = L.P[lane] + L.K[lane] + L.dxv[lane] + (ok ? 0.0 : 1.0);
 }
 
-// both forms on the same data: max |difference| of P' (every stage), K', Ru^-1 and the magnitudes
+// forward and corrector sweeps with PF = 1 and PF = 2 on the same data: max |difference|
 template <int ID>
 __global__ __launch_bounds__(64) void cmp(int H, double* out) {
     using K = SqpKernel<ID>;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const auto L = K::carve(smem, H);
     const int lane = threadIdx.x;
-    const int np = (H + 1) * K::PP, nk = H * K::NU * K::PS, nr = H * K::NU * K::NU;
-    init_stage_data<ID>(L, H, lane, 5);
-    K::template mfma_backward_h<false>(L, H, lane);
+    constexpr int NX = K::NX, PP = K::PP, PO = K::PO, NU = K::NU, PS = K::PS;
+    const int nd = (H + 1) * NX;
+    constexpr int CAP = 8;
+    double a[CAP], p[CAP], kf[CAP];
+    init_stage_data<ID>(L, H, lane, 3);
+    K::template mfma4_forward<1>(L, H, lane);
     __syncthreads();
-    constexpr int CAP = 24;
-    double a[CAP], b[CAP], c[CAP];
+    for (int q = 0; q < CAP; ++q) { const int e = lane + 64 * q; a[q] = e < nd ? L.dxv[e] : 0.0; }
+    __syncthreads();
+    K::template mfma4_forward<2>(L, H, lane);
+    __syncthreads();
+    double ef = 0.0;
+    for (int q = 0; q < CAP; ++q) { const int e = lane + 64 * q; if (e < nd) ef = fmax(ef, fabs(L.dxv[e] - a[q])); }
+    init_stage_data<ID>(L, H, lane, 4);
+    K::template mfma4_vector_backward<1>(L, H, lane);
+    __syncthreads();
     for (int q = 0; q < CAP; ++q) {
         const int e = lane + 64 * q;
-        a[q] = e < np ? L.P[e] : 0.0;
-        b[q] = e < nk ? L.K[e] : 0.0;
-        c[q] = e < nr ? L.Rui[e] : 0.0;
+        p[q] = e < nd ? L.P[(e / NX) * PP + PO + e % NX] : 0.0;
+        kf[q] = e < H * NU ? L.K[(e / NU) * NU * PS + (e % NU) * PS + NX] : 0.0;
     }
     __syncthreads();
-    init_stage_data<ID>(L, H, lane, 5);
-    K::template mfma_backward_h<true>(L, H, lane);
+    init_stage_data<ID>(L, H, lane, 4);
+    K::template mfma4_vector_backward<2>(L, H, lane);
     __syncthreads();
-    double ep = 0.0, ek = 0.0, er = 0.0, mp = 0.0, mk = 0.0;
+    double ev = 0.0;
     for (int q = 0; q < CAP; ++q) {
         const int e = lane + 64 * q;
-        if (e >= K::PP && e < np) { ep = fmax(ep, fabs(L.P[e] - a[q])); mp = fmax(mp, fabs(a[q])); }
-        if (e < nk) { ek = fmax(ek, fabs(L.K[e] - b[q])); mk = fmax(mk, fabs(b[q])); }
-        if (e < nr) er = fmax(er, fabs(L.Rui[e] - c[q]));
+        if (e < nd) ev = fmax(ev, fabs(L.P[(e / NX) * PP + PO + e % NX] - p[q]));
+        if (e < H * NU) ev = fmax(ev, fabs(L.K[(e / NU) * NU * PS + (e % NU) * PS + NX] - kf[q]));
     }
-    ep = wave_max(ep); ek = wave_max(ek); er = wave_max(er); mp = wave_max(mp); mk = wave_max(mk);
-    if (lane == 0) { out[0] = ep; out[1] = mp; out[2] = ek; out[3] = mk; out[4] = er; }
+    ef = wave_max(ef);
+    ev = wave_max(ev);
+    if (lane == 0) { out[0] = ef; out[1] = ev; }
 }
 
-template <int ID, bool HY>
+template <int ID, int V>
 static double run(const char* name, int H, int B, int reps, unsigned long long* d_out, double* d_sink) {
     const size_t lds = SqpKernel<ID>::lds_doubles(H) * sizeof(double);
-    micro<ID, HY><<<B, 64, lds>>>(H, reps, d_out, d_sink);
+    micro<ID, V><<<B, 64, lds>>>(H, reps, d_out, d_sink);
     (void)hipDeviceSynchronize();
-    micro<ID, HY><<<B, 64, lds>>>(H, reps, d_out, d_sink);
+    micro<ID, V><<<B, 64, lds>>>(H, reps, d_out, d_sink);
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> h(B);
     (void)hipMemcpy(h.data(), d_out, B * sizeof(unsigned long long), hipMemcpyDeviceToHost);
@@ -97,7 +116,7 @@ static double run(const char* name, int H, int B, int reps, unsigned long long* 
     for (auto v : h) mean += (double)v;
     mean /= B;
     const double per = mean / reps;
-    printf("%-34s H=%d: %9.0f cycles/factorisation  %7.1f cycles/stage\n", name, H, per, per / H);
+    printf("%-34s H=%d: %9.0f cycles/recursion  %7.1f cycles/stage\n", name, H, per, per / H);
     return per;
 }
 
@@ -108,8 +127,7 @@ static void check(const char* name, int H) {
     cmp<ID><<<1, 64, SqpKernel<ID>::lds_doubles(H) * sizeof(double)>>>(H, d);
     double h[8];
     (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    printf("check %s H=%d hybrid vs 16x16x4: P' %.3e (max %.3e)  K' %.3e (max %.3e)  Ru^-1 %.3e\n", name, H, h[0], h[1],
-           h[2], h[3], h[4]);
+    printf("check %s H=%d PF2 vs PF1: forward %.3e  corrector %.3e\n", name, H, h[0], h[1]);
     (void)hipFree(d);
 }
 
@@ -119,10 +137,16 @@ int main() {
     double* d_sink;
     (void)hipMalloc(&d_out, B * sizeof(unsigned long long));
     (void)hipMalloc(&d_sink, B * 8 * sizeof(double));
-    run<kQuad2D, false>("quad2d factor, 16x16x4", 30, B, reps, d_out, d_sink);
-    run<kQuad2D, true>("quad2d factor, hybrid 4x4x4_4b", 30, B, reps, d_out, d_sink);
-    run<kCartpole, false>("cartpole factor, 16x16x4", 20, B, reps, d_out, d_sink);
-    run<kCartpole, true>("cartpole factor, hybrid 4x4x4_4b", 20, B, reps, d_out, d_sink);
+    run<kQuad2D, 0>("quad2d factorisation", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 1>("quad2d forward, PF 1", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 2>("quad2d forward, PF 2", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 3>("quad2d corrector, PF 1", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 4>("quad2d corrector, PF 2", 30, B, reps, d_out, d_sink);
+    run<kCartpole, 0>("cartpole factorisation", 20, B, reps, d_out, d_sink);
+    run<kCartpole, 1>("cartpole forward, PF 1", 20, B, reps, d_out, d_sink);
+    run<kCartpole, 2>("cartpole forward, PF 2", 20, B, reps, d_out, d_sink);
+    run<kCartpole, 3>("cartpole corrector, PF 1", 20, B, reps, d_out, d_sink);
+    run<kCartpole, 4>("cartpole corrector, PF 2", 20, B, reps, d_out, d_sink);
     check<kQuad2D>("quad2d", 30);
     check<kCartpole>("cartpole", 20);
     return 0;
