@@ -28,11 +28,6 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
-// stage operands of the 4-block MFMA sweeps loaded 2 (default) or 1 stage ahead (A/B)
-#ifndef GPMPC_SWEEP_PF
-#define GPMPC_SWEEP_PF 2
-#endif
-
 namespace gpmpc {
 
 // Orders the LDS traffic of the (main) wave.  One wave per block: __syncthreads.  With GP helper
@@ -1216,9 +1211,6 @@ struct SqpKernel {
     // Forward sweep: dx_0 = 0, dx_{k+1} = A'_k [dx_k; 1]  (M_k = [A'_k; e_NX]).  Masked lanes read the
     // LDS zero slot (stride 0) and the homogeneous corner the one slot, so the stage operand is one
     // unconditional load issued a stage ahead.
-    // PF: stage operands loaded PF stages ahead (2: the LDS read of stage k + 2 has a whole stage to
-    // land, and the wait for it no longer sits on the recursion)
-    template <int PF = GPMPC_SWEEP_PF>
     __device__ static void mfma4_forward(const Lds& L, int H, int lane) {
         static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
         {
@@ -1232,31 +1224,15 @@ struct SqpKernel {
             const int ost = (stlo || sthi) ? NX : 0;
             if (lane < NX) L.dxv[lane] = 0.0;
             double y = mfma4_vec(q, [](int) { return 0.0; });
-            if constexpr (PF == 1) {
-                double an = *src;
-                for (int k = 0; k < H; ++k) {
-                    const double a = an;
-                    src += (k + 1 < H) ? st : 0;
-                    an = *src;
-                    double s;
-                    y = mfma4_stage(a, y, s);
-                    *out = s;
-                    out += ost;
-                }
-            } else {
-                double a0 = *src;
-                src += (1 < H) ? st : 0;
-                double a1 = *src;
-                for (int k = 0; k < H; ++k) {
-                    const double a = a0;
-                    a0 = a1;
-                    src += (k + 2 < H) ? st : 0;
-                    a1 = *src;   // stage k + 2 (the last stage again past the end)
-                    double s;
-                    y = mfma4_stage(a, y, s);
-                    *out = s;
-                    out += ost;
-                }
+            double an = *src;
+            for (int k = 0; k < H; ++k) {
+                const double a = an;
+                src += (k + 1 < H) ? st : 0;
+                an = *src;
+                double s;
+                y = mfma4_stage(a, y, s);
+                *out = s;
+                out += ost;
             }
         }
     }
@@ -1267,7 +1243,6 @@ struct SqpKernel {
     // with [q; r] = gq.  Only the p recurrence is sequential (one v_mfma_f64_4x4x4_4b + DPP merge per
     // stage, mfma4_stage); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
-    template <int PF = GPMPC_SWEEP_PF>   // stage operands PF stages ahead in the p recurrence (mfma4_forward)
     __device__ static void mfma4_vector_backward(const Lds& L, int H, int lane) {
         double* T = L.hq;
         double* VT = L.dxv;
@@ -1326,31 +1301,15 @@ struct SqpKernel {
             double* out = stlo ? L.P + (size_t)(H - 1) * PP + PO + q.r
                                : (sthi ? L.P + (size_t)(H - 1) * PP + PO + 4 + q.r : L.dummy + lane);
             const int ost = (stlo || sthi) ? PP : 0;
-            if constexpr (PF == 1) {
-                double an = *src;
-                for (int k = H - 1; k >= 0; --k) {
-                    const double a = an;
-                    src -= (k >= 1) ? st : 0;
-                    an = *src;
-                    double sv;
-                    y = mfma4_stage(a, y, sv);
-                    *out = sv;
-                    out -= ost;
-                }
-            } else {
-                double a0 = *src;
-                src -= (H >= 2) ? st : 0;
-                double a1 = *src;
-                for (int k = H - 1; k >= 0; --k) {
-                    const double a = a0;
-                    a0 = a1;
-                    src -= (k >= 2) ? st : 0;
-                    a1 = *src;   // stage k - 2 (stage 0 again past the end)
-                    double sv;
-                    y = mfma4_stage(a, y, sv);
-                    *out = sv;
-                    out -= ost;
-                }
+            double an = *src;
+            for (int k = H - 1; k >= 0; --k) {
+                const double a = an;
+                src -= (k >= 1) ? st : 0;
+                an = *src;
+                double sv;
+                y = mfma4_stage(a, y, sv);
+                *out = sv;
+                out -= ost;
             }
         }
         WSYNC();

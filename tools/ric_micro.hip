@@ -1,9 +1,10 @@
 // Micro-benchmark of the Newton-system recursions of SqpKernel<quad2d> / <cartpole> in isolation
 // (diagnostic only): the production device functions mfma_backward_h (factorisation),
 // mfma4_forward (forward sweep) and mfma4_vector_backward (corrector) on synthetic stage data in
-// LDS, one wave per instance, 1024 instances; the sweeps with their stage operands one (PF = 1) or
-// two (PF = 2) stages ahead, and an agreement check between the two.
-// (The round-4 hybrid factorisation it also timed lives in tools/hybrid_riccati_overlap.patch.)
+// LDS, one wave per instance, 1024 instances.  Round 4 also timed with it the hybrid factorisation
+// (tools/hybrid_riccati_overlap.patch; profiles/r4/ab_hybrid_overlap/ric_micro.txt) and the sweeps
+// with their stage operands two stages ahead instead of one (profiles/r4/ab_pf/ric_micro.txt): both
+// slower in the kernel and not kept.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 \
 //        -I gp-mpc_amd/csrc -o tools/ric_micro tools/ric_micro.hip
 #include <hip/hip_runtime.h>
@@ -37,7 +38,7 @@ __device__ void init_stage_data(const typename SqpKernel<ID>::Lds& L, int H, int
     __syncthreads();
 }
 
-// V: 0 factorisation, 1 forward PF1, 2 forward PF2, 3 corrector PF1, 4 corrector PF2
+// V: 0 factorisation, 1 forward sweep, 2 corrector (vector backward)
 template <int ID, int V>
 __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long* out, double* sink) {
     using K = SqpKernel<ID>;
@@ -49,58 +50,13 @@ __global__ __launch_bounds__(64) void micro(int H, int reps, unsigned long long*
     bool ok = true;
     for (int r = 0; r < reps; ++r) {
         if constexpr (V == 0) ok = K::mfma_backward_h(L, H, lane) && ok;
-        if constexpr (V == 1) K::template mfma4_forward<1>(L, H, lane);
-        if constexpr (V == 2) K::template mfma4_forward<2>(L, H, lane);
-        if constexpr (V == 3) K::template mfma4_vector_backward<1>(L, H, lane);
-        if constexpr (V == 4) K::template mfma4_vector_backward<2>(L, H, lane);
+        if constexpr (V == 1) K::mfma4_forward(L, H, lane);
+        if constexpr (V == 2) K::mfma4_vector_backward(L, H, lane);
         __syncthreads();
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     if (lane == 0) out[blockIdx.x] = t1 - t0;
     if (lane < K::NX) sink[blockIdx.x * 8 + lane] = L.P[lane] + L.K[lane] + L.dxv[lane] + (ok ? 0.0 : 1.0);
-}
-
-// forward and corrector sweeps with PF = 1 and PF = 2 on the same data: max |difference|
-template <int ID>
-__global__ __launch_bounds__(64) void cmp(int H, double* out) {
-    using K = SqpKernel<ID>;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const auto L = K::carve(smem, H);
-    const int lane = threadIdx.x;
-    constexpr int NX = K::NX, PP = K::PP, PO = K::PO, NU = K::NU, PS = K::PS;
-    const int nd = (H + 1) * NX;
-    constexpr int CAP = 8;
-    double a[CAP], p[CAP], kf[CAP];
-    init_stage_data<ID>(L, H, lane, 3);
-    K::template mfma4_forward<1>(L, H, lane);
-    __syncthreads();
-    for (int q = 0; q < CAP; ++q) { const int e = lane + 64 * q; a[q] = e < nd ? L.dxv[e] : 0.0; }
-    __syncthreads();
-    K::template mfma4_forward<2>(L, H, lane);
-    __syncthreads();
-    double ef = 0.0;
-    for (int q = 0; q < CAP; ++q) { const int e = lane + 64 * q; if (e < nd) ef = fmax(ef, fabs(L.dxv[e] - a[q])); }
-    init_stage_data<ID>(L, H, lane, 4);
-    K::template mfma4_vector_backward<1>(L, H, lane);
-    __syncthreads();
-    for (int q = 0; q < CAP; ++q) {
-        const int e = lane + 64 * q;
-        p[q] = e < nd ? L.P[(e / NX) * PP + PO + e % NX] : 0.0;
-        kf[q] = e < H * NU ? L.K[(e / NU) * NU * PS + (e % NU) * PS + NX] : 0.0;
-    }
-    __syncthreads();
-    init_stage_data<ID>(L, H, lane, 4);
-    K::template mfma4_vector_backward<2>(L, H, lane);
-    __syncthreads();
-    double ev = 0.0;
-    for (int q = 0; q < CAP; ++q) {
-        const int e = lane + 64 * q;
-        if (e < nd) ev = fmax(ev, fabs(L.P[(e / NX) * PP + PO + e % NX] - p[q]));
-        if (e < H * NU) ev = fmax(ev, fabs(L.K[(e / NU) * NU * PS + (e % NU) * PS + NX] - kf[q]));
-    }
-    ef = wave_max(ef);
-    ev = wave_max(ev);
-    if (lane == 0) { out[0] = ef; out[1] = ev; }
 }
 
 template <int ID, int V>
@@ -120,17 +76,6 @@ static double run(const char* name, int H, int B, int reps, unsigned long long* 
     return per;
 }
 
-template <int ID>
-static void check(const char* name, int H) {
-    double* d;
-    (void)hipMalloc(&d, 8 * sizeof(double));
-    cmp<ID><<<1, 64, SqpKernel<ID>::lds_doubles(H) * sizeof(double)>>>(H, d);
-    double h[8];
-    (void)hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
-    printf("check %s H=%d PF2 vs PF1: forward %.3e  corrector %.3e\n", name, H, h[0], h[1]);
-    (void)hipFree(d);
-}
-
 int main() {
     const int B = 1024, reps = 50;
     unsigned long long* d_out;
@@ -138,16 +83,10 @@ int main() {
     (void)hipMalloc(&d_out, B * sizeof(unsigned long long));
     (void)hipMalloc(&d_sink, B * 8 * sizeof(double));
     run<kQuad2D, 0>("quad2d factorisation", 30, B, reps, d_out, d_sink);
-    run<kQuad2D, 1>("quad2d forward, PF 1", 30, B, reps, d_out, d_sink);
-    run<kQuad2D, 2>("quad2d forward, PF 2", 30, B, reps, d_out, d_sink);
-    run<kQuad2D, 3>("quad2d corrector, PF 1", 30, B, reps, d_out, d_sink);
-    run<kQuad2D, 4>("quad2d corrector, PF 2", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 1>("quad2d forward sweep", 30, B, reps, d_out, d_sink);
+    run<kQuad2D, 2>("quad2d corrector", 30, B, reps, d_out, d_sink);
     run<kCartpole, 0>("cartpole factorisation", 20, B, reps, d_out, d_sink);
-    run<kCartpole, 1>("cartpole forward, PF 1", 20, B, reps, d_out, d_sink);
-    run<kCartpole, 2>("cartpole forward, PF 2", 20, B, reps, d_out, d_sink);
-    run<kCartpole, 3>("cartpole corrector, PF 1", 20, B, reps, d_out, d_sink);
-    run<kCartpole, 4>("cartpole corrector, PF 2", 20, B, reps, d_out, d_sink);
-    check<kQuad2D>("quad2d", 30);
-    check<kCartpole>("cartpole", 20);
+    run<kCartpole, 1>("cartpole forward sweep", 20, B, reps, d_out, d_sink);
+    run<kCartpole, 2>("cartpole corrector", 20, B, reps, d_out, d_sink);
     return 0;
 }

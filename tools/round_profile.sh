@@ -18,10 +18,10 @@ timeout -k 10 300 python3 tools/phase_timing.py --model quad3d --n-train 4000 --
     --var-inputs dynamics --warmup 3 --steps 3 > "$OUT/phase_timing_config5.txt" 2>&1
 timeout -k 10 240 python3 -u bench.py --model cartpole --n-train 50 --horizon 20 --batch 256 \
     --steps 20 --warmup 5 > "$OUT/config2.json" 2>> "$OUT/bench.err"
-timeout -k 10 300 python3 -u bench.py --n-train 1000 --steps 20 --warmup 5 > "$OUT/config4.json" 2>> "$OUT/bench.err"
+timeout -k 10 300 python3 -u bench.py --n-train 1000 --batch 1024 --steps 20 --warmup 5 > "$OUT/config4.json" 2>> "$OUT/bench.err"
 timeout -k 10 600 python3 -u bench.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
     --var-inputs dynamics --steps 20 --warmup 5 > "$OUT/config5.json" 2>> "$OUT/bench.err"
-timeout -k 10 300 python3 -u bench.py --n-train 1000 --steps 20 --warmup 5 --variance exact --no-cpu-baseline \
+timeout -k 10 300 python3 -u bench.py --n-train 1000 --batch 1024 --steps 20 --warmup 5 --variance exact --no-cpu-baseline \
     > "$OUT/config4_exact.json" 2>> "$OUT/bench.err"
 timeout -k 10 600 python3 -u bench.py --model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 \
     --var-inputs dynamics --steps 20 --warmup 5 --variance exact --no-cpu-baseline > "$OUT/config5_exact.json" 2>> "$OUT/bench.err"
