@@ -185,6 +185,10 @@ def parse_args(argv=None):
                          "'exact' = L^-1 k at every size")
     ap.add_argument("--pmc-summary", default=str(ROOT / "profiles" / "pmc_current.json"),
                     help="tools/pmc_summary.py output of the same command (roofline.traffic)")
+    ap.add_argument("--shard", default="",
+                    help="R/N: run only rank R's slice of the N-rank partition, in this one process on one GPU "
+                         "(measures one rank of a strong-scaled job; the job time is the max over its N shards, "
+                         "tools/shard_sweep.sh); value then counts this shard's instances")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal: host sleep instead of the GPU step (launcher / shards / timing)")
     return ap.parse_args(argv)
@@ -297,7 +301,8 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
     # one rank per GPU (local_rank modulo the visible GPUs only matters for a rehearsal of the
     # multi-rank path on fewer GPUs, with GPMPC_DIST_BACKEND=gloo)
     gpu = local_rank % max(torch.cuda.device_count(), 1)
-    dist = init_dist(world, gpu, use_gpu=True)
+    emulated = bool(args.shard)   # one rank of an N-rank job, alone (no process group)
+    dist = None if emulated else init_dist(world, gpu, use_gpu=True)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
@@ -391,8 +396,10 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
     ids = D.shard_slice(args.global_batch, rank, world) if args.global_batch else D.shard_range(args.batch, rank)
     total_instances = args.global_batch or args.batch * world
     m = measure(ids, total_instances)
+    if emulated:   # this shard's own throughput (the job's is the slowest shard's time over all of them)
+        m["value"] = len(ids) * args.steps / m["elapsed"]
     weak = None
-    if weak_secondary and world > 1:
+    if weak_secondary and world > 1 and not emulated:
         w = measure(D.shard_range(WEAK_BATCH, rank), WEAK_BATCH * world)
         weak = {"value": w["value"], "batch_per_gpu": WEAK_BATCH, "global_batch": WEAK_BATCH * world,
                 "ms_per_step": w["elapsed"] / args.steps * 1e3, "scaling": "weak",
@@ -429,7 +436,7 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         except (OSError, ValueError, KeyError):
             traffic = None
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:   # rank 0 at N=1 only
+        if world == 1 and not args.no_cpu_baseline and not emulated:   # rank 0 at N=1 only
             cpu = cpu_baseline(spec, data, hyp, H, args.cpu_seconds, lqr_mats, m["x0_all"], m["phase_all"], list(ids),
                                args.warmup, args.steps, fitc=fitc, love_roots=solver.love_roots, qp_tol=args.qp_tol)
         sq = np.array(sqp_list) if sqp_list else np.zeros(1)
@@ -489,6 +496,10 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
             "weak_per_gpu": weak,
             "cpu_baseline": cpu,
         }
+        if emulated:
+            out["emulated_shard"] = {"rank": rank, "world": world, "instances": [ids.start, ids.stop],
+                                     "note": "one rank of the N-rank partition run alone on one GPU; value = this "
+                                             "shard's instances x steps / its time"}
         print(json.dumps(out))
     if dist is not None:
         dist.barrier()
@@ -501,7 +512,14 @@ def main(argv=None):
     # N ranks without torchrun: relaunch under torch.distributed.run before touching the GPU
     maybe_spawn(args.gpus, str(Path(__file__).resolve()), argv)
     rank, local_rank, world = rank_env()
-    if world != args.gpus:
+    if args.shard:
+        if world != 1 or args.dry_run:
+            raise SystemExit("--shard R/N runs one rank alone: start it as a single process")
+        rank, world = (int(v) for v in args.shard.split("/"))
+        if not 0 <= rank < world:
+            raise SystemExit("--shard R/N needs 0 <= R < N")
+        args.gpus = world
+    elif world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     weak_secondary = resolve_partition(args)
     if args.dry_run:
