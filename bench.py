@@ -411,7 +411,7 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
     sqp_mean, lin_mean, qp_mean = m["sqp_mean"], m["lin_mean"], m["qp_mean"]
     status_counts, maxes = m["status_counts"], m["maxes"]
 
-    if rank == 0:
+    if rank == 0 or emulated:   # an emulated shard is the only process: it always reports
         per_lin, exps_lin, var_flops = gp_flops(spec, N, H, getattr(solver, "love_ranks", None))
         # dominant kernel: the SQP kernel; linearisations computed per instance-step = sqp_iter + 1,
         # minus the one read from the linearisation cache (lin_mean, counted by the kernel)
