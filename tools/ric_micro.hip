@@ -3,8 +3,9 @@
 // mfma4_forward (forward sweep) and mfma4_vector_backward (corrector) on synthetic stage data in
 // LDS, one wave per instance, 1024 instances.  Round 4 also timed with it the hybrid factorisation
 // (tools/hybrid_riccati_overlap.patch; profiles/r4/ab_hybrid_overlap/ric_micro.txt) and the sweeps
-// with their stage operands two stages ahead instead of one (profiles/r4/ab_pf/ric_micro.txt): both
-// slower in the kernel and not kept.
+// with their stage operands two stages ahead instead of one (profiles/r4/ab_pf/ric_micro.txt), and the
+// segmented forward sweep on the helper waves (tools/segmented_forward_sweep.patch, which also adds
+// its timing here; profiles/r4/ab_seg/ric_micro.txt): all slower in the kernel and not kept.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 \
 //        -I gp-mpc_amd/csrc -o tools/ric_micro tools/ric_micro.hip
 #include <hip/hip_runtime.h>
