@@ -14,6 +14,7 @@
 #include "models.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace gpmpc {
@@ -313,6 +314,144 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
     }
 }
 
+// ---------------------------------------------------------------------------- variance, N <= 256, few points
+// The same variance when the launch has too few points to fill the device (the tightening of the
+// strong-scaled shards: 128-256 instances, 30-60 workgroups of 128 points per GP): a wave of
+// gp_var_tri_kernel owns 16 points against every column tile of the triangle (364 dependent-free
+// but serially issued MFMAs at NT = 13), so a sparse launch lasts one wave's MFMA stream.  Here the
+// column tiles of a 16-point tile are split over S waves (snake order over the triangle's per-tile
+// work: 24 / 23 / 22 / 22 panels at NT = 13, S = 4), the workgroup's 8 waves covering 8/S point tiles:
+// S times the waves, each with 1/S of the MFMAs.  The kernel values are computed once per point
+// tile (wave cg takes K-steps cg, cg + S, ..) and exchanged through LDS one panel ahead, behind the
+// panel barrier the L^-T staging already has.  Each wave reduces its tiles' squared norms; the
+// S partial norms of a point are added in wave order (deterministic) by the tile's first wave.
+__host__ __device__ constexpr int split_owner(int t, int nt, int s) {
+    const int i = nt - 1 - t;   // position in descending per-tile work (tile t: t + 1 panels)
+    const int r = i / s, j = i % s;
+    return (r & 1) ? s - 1 - j : j;
+}
+
+template <int NT, bool FROM_STATE, int S, int CG>
+__device__ __forceinline__ void var_split_body(const GPDev& g, const PostArgs& a, double* panel, double* kvb,
+                                               double* red, int pt) {
+    constexpr int PT = kPostWaves / S;   // point tiles per workgroup
+    constexpr int W = 16 * (NT | 1);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int lc = lane & 15, kq = lane >> 4;
+    const int p0 = (blockIdx.x * PT + pt) * 16;
+    const int p = p0 + lc;
+    double z[3];
+    load_point<FROM_STATE>(a, p < a.P ? p : a.P - 1, z);
+    const double c = -0.5 * g.inv_ell2, sf2 = g.sf2;
+    constexpr int npad = 16 * NT;
+    const double4* rows = reinterpret_cast<const double4*>(g.vrows);
+    double2 stage[4];
+    auto fetch = [&](int q) {
+        const int w = 16 * (NT - q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 2 * (tid + j * 64 * kPostWaves);
+            const int row = e / w, col = e - row * w;
+            stage[j] = (row < 16) ? *reinterpret_cast<const double2*>(g.linvT + (size_t)(16 * q + row) * npad + 16 * q + col)
+                                  : double2{0.0, 0.0};
+        }
+    };
+    auto deposit = [&](int q, double* buf) {
+        const int w = 16 * (NT - q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int e = 2 * (tid + j * 64 * kPostWaves);
+            const int row = e / w, col = e - row * w;
+            if (row < 16) *reinterpret_cast<double2*>(buf + row * W + 16 * q + col) = stage[j];
+        }
+    };
+    // this wave's K-steps of panel q: exps into kvb[q & 1][pt][ks][lane]
+    auto kvals = [&](int q) {
+        double* dst = kvb + ((size_t)(q & 1) * PT + pt) * 4 * 64 + lane;
+#pragma unroll
+        for (int ks = CG; ks < 4; ks += S) {
+            const double4 rw = rows[16 * q + 4 * ks + kq];
+            const double d0 = rw.x - z[0], d1 = rw.y - z[1], d2 = rw.z - z[2];
+            dst[ks * 64] = sf2 * exp_rbf(c * fma(d0, d0, fma(d1, d1, d2 * d2)));
+        }
+    };
+    f64x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+    fetch(0);
+    kvals(0);
+    deposit(0, panel);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+        const double* buf = panel + (q & 1) * 16 * W;
+        double kv[4];
+        const double* src = kvb + ((size_t)(q & 1) * PT + pt) * 4 * 64 + lane;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) kv[ks] = src[ks * 64];
+        if (q + 1 < NT) {
+            fetch(q + 1);
+            kvals(q + 1);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const double* brow = buf + (4 * ks + kq) * W + lc;
+#pragma unroll
+            for (int t = q; t < NT; ++t)   // (unrolled: the ownership test folds)
+                if (split_owner(t, NT, S) == CG)
+                    acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(kv[ks], brow[16 * t], acc[t], 0, 0, 0);
+        }
+        if (q + 1 < NT) deposit(q + 1, panel + ((q + 1) & 1) * 16 * W);
+        __syncthreads();
+    }
+    double sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+        if (split_owner(t, NT, S) == CG) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sq[r] = fma(acc[t][r], acc[t][r], sq[r]);
+        }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sq[r] = dpp_row_sum(sq[r]);
+    if (lc == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((size_t)pt * S + CG) * 16 + kq + 4 * r] = sq[r];
+    }
+    __syncthreads();
+    if (CG == 0 && lane < 16) {
+        double v = 0.0;
+#pragma unroll
+        for (int w = 0; w < S; ++w) v += red[((size_t)pt * S + w) * 16 + lane];
+        const int pr = p0 + lane;
+        if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = sf2 - v + (a.with_noise ? g.sn2 : 0.0);
+    }
+}
+
+template <int NT, bool FROM_STATE, int S>
+__global__ __launch_bounds__(64 * kPostWaves) void gp_var_split_kernel(PostBatch pb) {
+    extern __shared__ __attribute__((aligned(16))) double panel[];
+    constexpr int PT = kPostWaves / S;
+    constexpr int W = 16 * (NT | 1);
+    const GPDev& g = pb.g[blockIdx.y];
+    const PostArgs& a = pb.a[blockIdx.y];
+    if ((int)blockIdx.x * PT * 16 >= a.P) return;   // uniform
+    double* kvb = panel + 2 * 16 * W;                // [2][PT][4][64]
+    double* red = kvb + 2 * PT * 4 * 64;             // [PT][S][16]
+    const int wave = threadIdx.x >> 6;
+    const int pt = wave / S, cg = wave % S;
+    static_assert(S == 4, "four column groups (the shipped split; two measured slower)");
+    switch (cg) {   // wave-uniform: the column ownership is compile-time inside each body
+        case 0: var_split_body<NT, FROM_STATE, S, 0>(g, a, panel, kvb, red, pt); break;
+        case 1: var_split_body<NT, FROM_STATE, S, 1>(g, a, panel, kvb, red, pt); break;
+        case 2: var_split_body<NT, FROM_STATE, S, 2>(g, a, panel, kvb, red, pt); break;
+        default: var_split_body<NT, FROM_STATE, S, 3>(g, a, panel, kvb, red, pt); break;
+    }
+}
+__host__ __device__ constexpr int var_split_lds(int nt, int s) {
+    return (2 * 16 * 16 * (nt | 1) + 2 * (kPostWaves / s) * 4 * 64 + kPostWaves * 16) * (int)sizeof(double);
+}
+
 // ---------------------------------------------------------------------------- variance, LOVE root
 // var(z) = sf2 - ||R^T k(z, X)||^2 (+ sn2) with the dense LOVE root R [npad][rank, padded to 16]
 // (gpytorch fast_pred_var, rank <= 100 for configs 4/5).  No LDS and no barriers: one wavefront =
@@ -466,9 +605,24 @@ hipError_t launch_love(const PostBatch& pb, hipStream_t stream) {
 }
 
 template <bool FROM_STATE, int NT = 1>
-hipError_t launch_var_tri(const PostBatch& pb, int ntile, int blocks, hipStream_t stream) {
+hipError_t launch_var_tri(const PostBatch& pb, int ntile, int blocks, int split, hipStream_t stream) {
     if constexpr (NT <= kMaxCT) {
         if (ntile == NT) {
+            if (split == 4) {   // few points: column tiles over four waves per point tile
+                static bool sattr = false;
+                const int lds = var_split_lds(NT, split);
+                auto* k = gp_var_split_kernel<NT, FROM_STATE, 4>;
+                if (!sattr) {
+                    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                    if (e != hipSuccess) return e;
+                    sattr = true;
+                }
+                const int pts = 16 * (kPostWaves / split);
+                int sblocks = 0;
+                for (int q = 0; q < pb.n; ++q) sblocks = std::max(sblocks, (pb.a[q].P + pts - 1) / pts);
+                hipLaunchKernelGGL(k, dim3(sblocks, pb.n), dim3(64 * kPostWaves), lds, stream, pb);
+                return hipGetLastError();
+            }
             static bool attr = false;
             const int lds = 2 * 16 * 16 * (NT | 1) * (int)sizeof(double);
             if (!attr) {
@@ -481,7 +635,7 @@ hipError_t launch_var_tri(const PostBatch& pb, int ntile, int blocks, hipStream_
                                stream, pb);
             return hipGetLastError();
         }
-        return launch_var_tri<FROM_STATE, NT + 1>(pb, ntile, blocks, stream);
+        return launch_var_tri<FROM_STATE, NT + 1>(pb, ntile, blocks, split, stream);
     }
     return hipErrorInvalidValue;
 }
@@ -510,8 +664,24 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
         tri = tri && pb.a[q].mean == nullptr && pb.a[q].var != nullptr && pb.g[q].linvT != nullptr &&
               pb.g[q].vroot == nullptr && pb.npad[q] == pb.npad[0] && pb.npad[q] <= 16 * kMaxCT;
     if (tri) {
-        return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, stream)
-                          : launch_var_tri<false>(pb, pb.npad[0] / 16, blocks, stream);
+        // column split over four waves when the 128-point workgroups would fill at most half the CUs
+        // (measured, profiles/r4/ab_varsplit/: 128 quad2d instances 35.9 -> 19.7 us, 256: 36.5 -> 28.5 us,
+        // cartpole 256: 10.1 -> 9.0 us; at 512 and 1024 instances the split is slower: 38 -> 42 / 51 us,
+        // 71 -> 77 us; two waves per point tile measured between the two, eight: 128 instances 19 us,
+        // 256: 33 us, ab_varsplit8/).  GPMPC_VAR_SPLIT=1/4 forces a choice (A/B runs).
+        static int ncu = 0, force = -1;
+        if (ncu == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+                ncu = 256;
+            const char* f = std::getenv("GPMPC_VAR_SPLIT");
+            force = f ? std::atoi(f) : -1;
+        }
+        const int wgs = blocks * pb.n;
+        int split = 2 * wgs <= ncu ? 4 : 1;
+        if (force == 1 || force == 4) split = force;
+        return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, split, stream)
+                          : launch_var_tri<false>(pb, pb.npad[0] / 16, blocks, split, stream);
     }
     static bool attr = false;
     if (!attr) {

@@ -45,6 +45,41 @@ def test_gp_predict_matches_oracle(name, N):
         assert np.abs(v - vo).max() <= 1e-9 * gpo[g].sf2, (g, np.abs(v - vo).max())
 
 
+@pytest.mark.parametrize("name,N,H,B", [("quad2d", 200, 30, 16), ("quad2d", 200, 30, 512), ("quad2d", 200, 30, 1024),
+                                         ("cartpole", 50, 20, 256), ("quad2d", 17, 10, 3)])
+def test_tightening_variance_matches_oracle(name, N, H, B):
+    """The variance launch of the tightening (gp_var_tri_kernel, or gp_var_split_kernel with the column
+    tiles over four waves when the 128-point workgroups would fill at most half the CUs: B = 16, 3 and
+    cartpole's 256 here; quad2d at 512 and 1024 keeps one wave per point tile) at the previous
+    solution's points, read back
+    with gpmpc_get_variance, vs the oracle's variance with the likelihood noise:
+    |v - v_oracle| <= 1e-9 sf2."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(name, N)
+    gpo = oracle_gps(data, hyp)
+    gs = BatchSolver(spec, H, B)
+    gs.set_gps(product_gps(data, hyp))
+    gs.set_tightening(True, 0.95, *lqr(spec))
+    gs.reset(reset_iterate=True)
+    x0, ph = initial_states(spec, spec.reference_trajectory(), B)
+    obs = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    gs.solve(obs, ts)                                   # marks a previous solution
+    rng = np.random.default_rng(11)
+    xs = x0[:, None, :] + 0.1 * rng.standard_normal((B, H + 1, spec.nx))
+    us = 0.1 * rng.standard_normal((B, H, spec.nu))
+    gs.set_iterate(torch.tensor(xs, device="cuda"), torch.tensor(us, device="cuda"))
+    gs.solve(obs, ts)                                   # variance launch at (xs, us)
+    v = gs.variance().cpu().numpy()                     # (B, H, n_gp)
+    z = np.concatenate([xs[:, :H, :], us], axis=2)      # z_k = [x_k; u_k]
+    for g, idx in enumerate(spec.var_inputs):
+        vo = gpo[g].var(z[:, :, list(idx)].reshape(B * H, len(idx)), with_noise=True).reshape(B, H)
+        err = np.abs(v[:, :, g] - vo).max()
+        assert err <= 1e-9 * gpo[g].sf2, (g, err)
+
+
 @pytest.mark.parametrize("name,N,M", [("quad2d", 200, None), ("quad2d", 17, None), ("cartpole", 50, None),
                                       ("quad3d", 120, 60)])
 def test_linearisation_gp_mean_grad_matches_oracle(name, N, M):
