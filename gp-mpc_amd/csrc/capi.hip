@@ -103,6 +103,11 @@ struct gpmpc_handle {
     // stream first waits for it (order_after_last), so consecutive calls never overlap
     hipStream_t last_stream = nullptr;
     bool last_stream_valid = false;
+    // overlapped steps (gpmpc_solve): the second half's variance and SQP launches run on `side`,
+    // forked from and joined back into the caller's stream by two events
+    bool overlap = true;
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // The handle's device state (iterate, multipliers, variances, dispatch order) is read and written
@@ -146,6 +151,9 @@ static void free_handle(gpmpc_handle* h) {
     for (hipEvent_t e : h->ev_var_owned) h->ev_pool.push_back(e);
     for (auto& pr : h->ev_sqp) { h->ev_pool.push_back(pr.first); h->ev_pool.push_back(pr.second); }
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->side) (void)hipStreamDestroy(h->side);
     for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain, h->lin})
         if (p) (void)hipFree(p);
     if (h->has_prev) (void)hipFree(h->has_prev);
@@ -242,8 +250,10 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
         P.waves = ew ? std::atoi(ew) : 0;
         if (P.waves != 1 && P.waves != 2 && P.waves != 4) P.waves = 0;
         if (model_id == kQuad3D) P.waves = 0;             // quad3d always runs its four waves
-        const char* eo = std::getenv("GPMPC_ORDER");       // "0": dispatch in instance order (A/B)
-        P.order_dispatch = (eo && eo[0] == '0') ? 0 : 1;
+        const char* eo = std::getenv("GPMPC_ORDER");       // "0": instance order, "2": rank every launch (A/B)
+        P.order_dispatch = (eo && eo[0] == '0') ? 0 : ((eo && eo[0] == '2') ? 2 : 1);
+        const char* ov = std::getenv("GPMPC_OVERLAP");     // "0": one variance launch, then one SQP launch (A/B)
+        h->overlap = !(ov && ov[0] == '0');
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
         P.n_cu = ncu;
@@ -587,17 +597,12 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         if (e) h->ev_pool.push_back(e);
         e = nullptr;
     };
-    // 1. GP variances at the previous solution (the MFMA contraction), only when needed
-    hipEvent_t e0 = nullptr, e1 = nullptr, mid = nullptr;
-    const bool var_launch = P.tighten && h->any_prev;
-    if (var_launch) {
-        if (h->profiling) {
-            e0 = take_event(h);
-            e1 = take_event(h);
-            if (e0 && hipEventRecord(e0, s) != hipSuccess) give_back(e0);
-        }
+    // GP variances at the previous solution (the MFMA contraction) of the instances of ranks
+    // first .. first + count - 1 in `order` (null: instances first .. first + count - 1)
+    auto launch_var = [&](int first, int count, const int32_t* order, hipStream_t st) -> hipError_t {
         PostBatch pb{};
         pb.n = h->md.ngp;
+        pb.step_points = batch * h->H;
         for (int g = 0; g < h->md.ngp; ++g) {
             PostArgs& a = pb.a[g];
             a.sx = h->x;
@@ -608,20 +613,103 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             a.ngp = h->md.ngp;
             a.gp_index = g;
             for (int k = 0; k < 3; ++k) a.src[k] = h->md.var_src[g][k];
-            a.P = batch * h->H;
+            a.P = count * h->H;
             a.d = h->md.gp_dim[g];
             a.with_noise = 1;   // gp.likelihood(gp(z)) (gpmpc.py:444)
             a.mean = nullptr;
             a.var = h->var;
             a.var_stride = h->md.ngp;
             a.var_off = g;
+            a.order = order;
+            a.first = first;
             pb.g[g] = P.gp[g];
             pb.g[g].vroot = h->gp_vroot[g];   // LOVE (fast_pred_var) when a root is set
             pb.g[g].vroot_cols = h->gp_vroot_cols[g];
             pb.g[g].vroot_rank = h->gp_vroot_rank[g];
             pb.npad[g] = h->gp_npad[g];
         }
-        const hipError_t ve = launch_gp_post_batch(pb, true, s);
+        return launch_gp_post_batch(pb, true, st);
+    };
+    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag,
+               h->order, h->cost, 0};
+    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing, h->stats};
+    // optional outputs go to handle-owned scratch when NULL
+    if (!io.sqp_iter) io.sqp_iter = h->scratch_i;
+    if (!io.qp_iter) io.qp_iter = h->scratch_i + h->max_batch;
+    if (!io.res) io.res = h->scratch_d;
+    hipEvent_t e0 = nullptr, e1 = nullptr, mid = nullptr;
+    const bool var_launch = P.tighten && h->any_prev;
+
+    // Overlapped step: when the variance launch precedes an SQP launch that fills the device with one
+    // wave per instance (or needs more than one round of workgroups), the instances are ranked by
+    // the cost of their last solve and split in two halves.  The costlier half's variances run
+    // first and its SQP launch starts right after them; the cheaper half's variances and SQP launch
+    // run on a second stream beside it, so the step waits only for the first half's variances before
+    // the solves that set its length begin.  Each instance's arithmetic is unchanged (same kernels,
+    // same per-instance data), so the results are bit-identical to the sequential order.
+    if (var_launch && h->overlap && batch >= 2 && batch <= 16384 && sqp_overlap_ok(P, batch)) {
+        if (!h->side) {
+            int lo = 0, hi = 0;
+            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+            HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, lo));   // lowest priority
+            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+        }
+        const int b1 = (batch + 1) / 2, b2 = batch - b1;
+        HIPCHK(launch_sqp_order(S, batch, s));
+        if (h->profiling) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (e0 && hipEventRecord(e0, s) != hipSuccess) give_back(e0);
+        }
+        hipError_t ve = launch_var(0, b1, h->order, s);
+        if (ve == hipSuccess && e0 && e1 && hipEventRecord(e1, s) == hipSuccess) {
+            h->ev_var.push_back({e0, e1});
+            mid = e1;
+        } else {
+            give_back(e0);
+            give_back(e1);
+        }
+        if (ve == hipSuccess) ve = hipEventRecord(h->ev_fork, s);
+        if (ve == hipSuccess) ve = hipStreamWaitEvent(h->side, h->ev_fork, 0);
+        if (ve != hipSuccess) {
+            h->var_batch = 0;
+            if (mid) h->ev_var_owned.push_back(mid);
+            return fail(GPMPC_ERR_HIP, std::string("variance launch: ") + hipGetErrorString(ve));
+        }
+        h->var_batch = batch;
+        hipEvent_t e2 = h->profiling && mid ? take_event(h) : nullptr;
+        hipError_t le = launch_sqp(P, S, io, batch, s, 0, b1);
+        if (le == hipSuccess) le = launch_var(b1, b2, h->order, h->side);
+        if (le == hipSuccess) le = launch_sqp(P, S, io, batch, h->side, b1, b2);
+        // the join is recorded whatever happened above, so the caller's stream never runs ahead of
+        // work already queued on the side stream
+        const hipError_t je = hipEventRecord(h->ev_join, h->side);
+        const hipError_t we = je == hipSuccess ? hipStreamWaitEvent(s, h->ev_join, 0) : je;
+        if (le == hipSuccess) le = we;
+        if (le != hipSuccess) {
+            if (mid) h->ev_var_owned.push_back(mid);
+            give_back(e2);
+            return fail(GPMPC_ERR_HIP, std::string("launch_sqp: ") + hipGetErrorString(le));
+        }
+        h->any_prev = true;
+        if (mid && e2 && hipEventRecord(e2, s) == hipSuccess) {
+            h->ev_sqp.push_back({mid, e2});
+        } else {
+            if (mid) h->ev_var_owned.push_back(mid);
+            give_back(e2);
+        }
+        return GPMPC_OK;
+    }
+
+    // 1. GP variances at the previous solution, only when needed
+    if (var_launch) {
+        if (h->profiling) {
+            e0 = take_event(h);
+            e1 = take_event(h);
+            if (e0 && hipEventRecord(e0, s) != hipSuccess) give_back(e0);
+        }
+        const hipError_t ve = launch_var(0, batch, nullptr, s);
         if (ve != hipSuccess) {
             give_back(e0);
             give_back(e1);
@@ -638,13 +726,6 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     }
     h->var_batch = var_launch ? batch : 0;
     // 2. the SQP step
-    StateDev S{h->x, h->u, h->pi, h->lam, h->has_prev, h->var, h->tight, h->lin_cache ? h->lin : nullptr, h->lin_tag,
-               h->order, h->cost};
-    StepIO io{x0, tstep, u0, status, sqp_iter, qp_iter, res, h->timing, h->stats};
-    // optional outputs go to handle-owned scratch when NULL
-    if (!io.sqp_iter) io.sqp_iter = h->scratch_i;
-    if (!io.qp_iter) io.qp_iter = h->scratch_i + h->max_batch;
-    if (!io.res) io.res = h->scratch_d;
     e0 = e1 = nullptr;
     if (h->profiling) {
         e0 = mid;

@@ -25,7 +25,8 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 template <bool FROM_STATE>
 __device__ __forceinline__ void load_point(const PostArgs& a, int p, double (&z)[3]) {
     if (FROM_STATE) {
-        const int b = p / a.H, k = p % a.H;
+        const int r = p / a.H, k = p - r * a.H;
+        const int b = a.order ? a.order[a.first + r] : r;
 #pragma unroll
         for (int dd = 0; dd < 3; ++dd) {
             const int s = a.src[dd];
@@ -212,7 +213,7 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_post_kernel(PostBatch pb) 
                 const int pr = p0 + kq + 4 * r;
                 if (pr < a.P) {
                     const double v = g.sf2 - sq[r] + (a.with_noise ? g.sn2 : 0.0);
-                    a.var[(size_t)pr * a.var_stride + a.var_off] = v;
+                    a.var[post_row(a, pr) * a.var_stride + a.var_off] = v;
                 }
             }
         }
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(64 * kPostWaves) void gp_var_tri_kernel(PostBatch p
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int pr = p0 + kq + 4 * r;
-            if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = sf2 - sq[r] + (a.with_noise ? g.sn2 : 0.0);
+            if (pr < a.P) a.var[post_row(a, pr) * a.var_stride + a.var_off] = sf2 - sq[r] + (a.with_noise ? g.sn2 : 0.0);
         }
     }
 }
@@ -424,7 +425,7 @@ __device__ __forceinline__ void var_split_body(const GPDev& g, const PostArgs& a
 #pragma unroll
         for (int w = 0; w < S; ++w) v += red[((size_t)pt * S + w) * 16 + lane];
         const int pr = p0 + lane;
-        if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = sf2 - v + (a.with_noise ? g.sn2 : 0.0);
+        if (pr < a.P) a.var[post_row(a, pr) * a.var_stride + a.var_off] = sf2 - v + (a.with_noise ? g.sn2 : 0.0);
     }
 }
 
@@ -566,7 +567,7 @@ __device__ __forceinline__ void love_points(const GPDev& g, const PostArgs& a, i
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int pr = p0 + kq + 4 * r;
-            if (pr < a.P) a.var[(size_t)pr * a.var_stride + a.var_off] = g.sf2 - sf2sq * sq[r] + (a.with_noise ? g.sn2 : 0.0);
+            if (pr < a.P) a.var[post_row(a, pr) * a.var_stride + a.var_off] = g.sf2 - sf2sq * sq[r] + (a.with_noise ? g.sn2 : 0.0);
         }
     }
 }
@@ -677,7 +678,8 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
             const char* f = std::getenv("GPMPC_VAR_SPLIT");
             force = f ? std::atoi(f) : -1;
         }
-        const int wgs = blocks * pb.n;
+        const int step_blocks = pb.step_points > 0 ? (pb.step_points + 16 * kPostWaves - 1) / (16 * kPostWaves) : blocks;
+        const int wgs = step_blocks * pb.n;   // the split choice follows the whole step (bit-identical halves)
         int split = 2 * wgs <= ncu ? 4 : 1;
         if (force == 1 || force == 4) split = force;
         return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, split, stream)

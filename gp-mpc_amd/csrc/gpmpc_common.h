@@ -83,7 +83,7 @@ struct ProblemDev {
     int32_t waves;
     int32_t n_cu;             // compute units of the device (set by gpmpc_create)
     // cost-ordered dispatch (StateDev::order): on when a launch has more instances than the
-    // device holds at once (GPMPC_ORDER=0 turns it off, for A/B)
+    // device holds at once (GPMPC_ORDER=0 turns it off, =2 ranks every launch, for A/B)
     int32_t order_dispatch;
     GPDev gp[kMaxGP];
 };
@@ -113,6 +113,9 @@ struct StateDev {
     // barely changes from one control step to the next).  NULL: identity.
     const int32_t* order;
     uint32_t* cost;      // [B]
+    // rank of this launch's first workgroup in order[] (a launch over ranks first .. first + grid - 1:
+    // the two halves of an overlapped step, capi.hip gpmpc_solve); 0 otherwise
+    int32_t first;
 };
 
 struct StepIO {
@@ -144,7 +147,18 @@ struct PostArgs {
     double* mean;         // [P] or null
     double* var;          // var[p * var_stride + var_off] or null
     int32_t var_stride, var_off;
+    // gathered points only: point p is stage p % H of the instance of rank first + p / H in order[]
+    // (var row: that instance's), or of instance p / H when order is null
+    const int32_t* order;
+    int32_t first;
 };
+
+// var row of point p (see PostArgs::order)
+__device__ __forceinline__ size_t post_row(const PostArgs& a, int p) {
+    if (a.order == nullptr) return (size_t)p;
+    const int r = p / a.H;
+    return (size_t)a.order[a.first + r] * a.H + (p - r * a.H);
+}
 
 // exp(x) for the RBF kernel, x <= 0 and finite: Cody-Waite reduction x = n ln2 + r, |r| <= ln2/2,
 // degree-11 Chebyshev fit of exp on [-ln2/2, ln2/2] (mpmath chebyfit, fit error 3.2e-18; max
@@ -214,10 +228,17 @@ struct PostBatch {
     PostArgs a[kMaxGP];
     int32_t npad[kMaxGP];
     int32_t n;
+    // points of the whole step when this launch is one part of it (the overlapped halves): the
+    // kernel choice follows the step, so both halves use the kernel a single launch would (0: P)
+    int32_t step_points;
 };
 
 // Launchers (sqp_kernel.hip, gp_kernels.hip).
-hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream);
+// count < 0: the whole batch; else ranks first .. first + count - 1 of order[] (launch_sqp_order)
+hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
+                      int first = 0, int count = -1);
+hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream);
+bool sqp_overlap_ok(const ProblemDev& P, int batch);
 size_t sqp_lds_bytes(int model, int H);
 int model_unc_dims(int model, int32_t* unc);   // the model's uncertain state dims (Bd columns), returns their count
 hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* mean, double* grad, hipStream_t stream);

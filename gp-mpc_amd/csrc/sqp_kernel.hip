@@ -1420,7 +1420,7 @@ struct SqpKernel {
     template <bool SPL, int NV>
     __device__ static void dyn_residual_q(const Lds& L, int H, int kq, const double (&d)[NV], const double (&c)[NX],
                                           double (&r)[NX]) {
-        const int lane = threadIdx.x;
+        const int lane = threadIdx.x & 63;
         // full stage vectors of stages kq and kq + 1, by lane moves without the LDS crossbar: the
         // other half of the stage is lane ^ 32 (permlane32 swap), the next stage is lane + 1 of the
         // same half (DPP wave_shl:1; lanes whose source is past the end are unused stages)
@@ -1892,7 +1892,7 @@ struct SqpKernel {
     __device__ static void run(const ProblemDev& P, const StateDev& S, const StepIO& io) {
         const int H = P.H;
         const int lane = threadIdx.x & 63;
-        const int b = S.order ? __builtin_amdgcn_readfirstlane(S.order[blockIdx.x]) : (int)blockIdx.x;
+        const int b = S.order ? __builtin_amdgcn_readfirstlane(S.order[S.first + blockIdx.x]) : (int)blockIdx.x;
         extern __shared__ __attribute__((aligned(16))) double smem[];
         const Lds L = carve(smem, H);
         if constexpr (NWAVES > 1) {
@@ -2371,9 +2371,11 @@ template <int ID, int NW, bool SPL>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
     SqpKernel<ID, NW>::template run<SPL>(P, S, io);
 }
-
+// count < 0: the whole batch (ordered by cost here when it needs more than one round of workgroups);
+// count >= 0: ranks first .. first + count - 1 of an order[] launch_sqp_order already filled
 template <int ID, int NW, bool SPL>
-hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
+                              int first, int count) {
     const size_t lds = SqpKernel<ID, NW>::lds_doubles(P.H) * sizeof(double);
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL>,
@@ -2383,10 +2385,17 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
     // instances resident at once: one wave per SIMD (4 / NW per CU), bounded by the CU's 160 KB LDS
     const int per_cu = std::max(1, std::min(4 / NW, (int)((160 * 1024) / lds)));
     StateDev Sl = S;
+    Sl.first = 0;
+    if (count >= 0) {   // a chunk of ranks of the order already computed
+        if (count == 0) return hipSuccess;
+        Sl.first = first;
+        hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL>), dim3(count), dim3(64 * NW), lds, stream, P, Sl, io);
+        return hipGetLastError();
+    }
     // (rank by counting: O(B^2) comparisons, a few microseconds up to ~16 k instances; larger
     // launches keep instance order rather than pay for it)
-    if (S.order != nullptr && S.cost != nullptr && P.order_dispatch && P.n_cu > 0 && batch > P.n_cu * per_cu &&
-        batch <= 16384) {
+    if (S.order != nullptr && S.cost != nullptr && P.order_dispatch && P.n_cu > 0 &&
+        (batch > P.n_cu * per_cu || P.order_dispatch == 2) && batch <= 16384) {
         hipLaunchKernelGGL(order_by_cost_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, S.cost, batch,
                            const_cast<int32_t*>(S.order));
         const hipError_t e = hipGetLastError();
@@ -2414,20 +2423,59 @@ int sqp_waves(const ProblemDev& P, int batch) {
 }
 
 template <int ID>
-hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
+                           int first, int count) {
     if constexpr (kDefaultWaves<ID> == 1) {
         // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
         const bool spl = P.H + 1 <= 32;
-        const int nw = sqp_waves<ID>(P, batch);
+        const int nw = sqp_waves<ID>(P, batch);   // from the whole batch, also for a chunk of it
         if (nw == 4)
-            return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream);
+            return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream, first, count)
+                       : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream, first, count);
         if (nw == 2)
-            return spl ? launch_sqp_variant<ID, 2, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 2, false>(P, S, io, batch, stream);
-        return spl ? launch_sqp_variant<ID, 1, true>(P, S, io, batch, stream) : launch_sqp_variant<ID, 1, false>(P, S, io, batch, stream);
+            return spl ? launch_sqp_variant<ID, 2, true>(P, S, io, batch, stream, first, count)
+                       : launch_sqp_variant<ID, 2, false>(P, S, io, batch, stream, first, count);
+        return spl ? launch_sqp_variant<ID, 1, true>(P, S, io, batch, stream, first, count)
+                   : launch_sqp_variant<ID, 1, false>(P, S, io, batch, stream, first, count);
     } else {
         // multi-wave models split the IPM state over their waves instead (WSPL)
-        return launch_sqp_variant<ID, kDefaultWaves<ID>, false>(P, S, io, batch, stream);
+        return launch_sqp_variant<ID, kDefaultWaves<ID>, false>(P, S, io, batch, stream, first, count);
     }
+}
+
+// Whether a step of `batch` instances runs as two overlapped halves (gpmpc_solve): when its SQP
+// launch needs more than one round of workgroups (config 5: 512 quad3d instances, one per CU).
+// A launch that fits the device at once runs its instances side by side, and there the halves were
+// measured slower (profiles/r4/ab_overlap/: config 3 0.609 -> 0.933 ms per step, config 4 1.155 ->
+// 1.706): the costlier half then shares its CUs' LDS and instruction traffic with other costly
+// instances for the whole step instead of with instances that finish early.
+template <int ID>
+static bool overlap_ok_of(const ProblemDev& P, int batch) {
+    if (P.n_cu <= 0) return false;
+    const int nw = sqp_waves<ID>(P, batch);
+    size_t lds = SqpKernel<ID>::lds_doubles(P.H);
+    if constexpr (kDefaultWaves<ID> == 1) {
+        if (nw == 4) lds = SqpKernel<ID, 4>::lds_doubles(P.H);
+        if (nw == 2) lds = SqpKernel<ID, 2>::lds_doubles(P.H);
+    }
+    const int per_cu = std::max(1, std::min(4 / nw, (int)((160 * 1024) / (lds * sizeof(double)))));
+    return batch > P.n_cu * per_cu;
+}
+bool sqp_overlap_ok(const ProblemDev& P, int batch) {
+    switch (P.model) {
+        case kQuad2D: return overlap_ok_of<kQuad2D>(P, batch);
+        case kQuad3D: return overlap_ok_of<kQuad3D>(P, batch);
+        case kCartpole: return overlap_ok_of<kCartpole>(P, batch);
+    }
+    return false;
+}
+
+// order[] = the instances by decreasing cost of their last solve
+hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream) {
+    if (batch > 16384) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(order_by_cost_kernel, dim3((batch + 255) / 256), dim3(256), 0, stream, S.cost, batch,
+                       const_cast<int32_t*>(S.order));
+    return hipGetLastError();
 }
 
 template <int ID>
@@ -2459,11 +2507,12 @@ size_t sqp_lds_bytes(int model, int H) {
     return 0;
 }
 
-hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream) {
+hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
+                      int first, int count) {
     switch (P.model) {
-        case kQuad2D: return launch_sqp_step<kQuad2D>(P, S, io, batch, stream);
-        case kQuad3D: return launch_sqp_step<kQuad3D>(P, S, io, batch, stream);
-        case kCartpole: return launch_sqp_step<kCartpole>(P, S, io, batch, stream);
+        case kQuad2D: return launch_sqp_step<kQuad2D>(P, S, io, batch, stream, first, count);
+        case kQuad3D: return launch_sqp_step<kQuad3D>(P, S, io, batch, stream, first, count);
+        case kCartpole: return launch_sqp_step<kCartpole>(P, S, io, batch, stream, first, count);
     }
     return hipErrorInvalidValue;
 }

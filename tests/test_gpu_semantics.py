@@ -248,3 +248,44 @@ def test_variance_readback_only_after_a_variance_launch():
     gs.reset(reset_iterate=False)
     with pytest.raises(_lib.GPMPCError):
         gs.variance()
+
+
+@pytest.mark.parametrize("model,H,n,B", [("quad2d", 30, 200, 1100), ("cartpole", 20, 50, 1100), ("quad3d", 12, 60, 300)])
+def test_overlapped_step_is_bit_exact(model, H, n, B, monkeypatch):
+    """A step whose SQP launch needs more than one round of workgroups (more instances than the
+    device holds at once: 4 per CU for the one-wave models here, 1 for quad3d) runs as two
+    cost-ranked halves, the second half's variance and SQP launches on a side stream beside the
+    first half's SQP launch (gpmpc_solve).
+    Against a solver with the overlap off (GPMPC_OVERLAP=0: one variance launch, then one SQP
+    launch) every output, the iterate and the tightening variances are bit-identical over a closed
+    loop (the ranking changes from step to step with the instances' costs)."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(model, n)
+    mats = lqr(spec)
+
+    def make():
+        s = BatchSolver(spec, H, B)
+        s.set_gps(product_gps(data, hyp))
+        s.set_tightening(True, 0.95, *mats)
+        s.reset(reset_iterate=True)
+        return s
+
+    on = make()
+    monkeypatch.setenv("GPMPC_OVERLAP", "0")
+    off = make()
+    monkeypatch.delenv("GPMPC_OVERLAP")
+    x0, ph = initial_states(spec, spec.reference_trajectory(), B)
+    x = torch.tensor(x0, device="cuda")
+    ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
+    for k in range(5):
+        outs = []
+        for s in (on, off):
+            u = s.solve(x, ts + k).clone()
+            outs.append((u, s.status.clone(), s.sqp_iter.clone(), s.qp_iter.clone(), s.res.clone(), *s.solution()[:2]))
+            if k >= 1:
+                outs[-1] = outs[-1] + (s.variance().clone(),)
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), k
+        x = on.plant_step(x, outs[0][0], ts + k)

@@ -1,27 +1,31 @@
 #!/bin/bash
-# Cost-ordered dispatch A/B (round 3): config 5 (512 instances, one per CU: two rounds) with the
-# ordering on / off (GPMPC_ORDER=0) and the previous commit's library; config 3 (one round, no
-# ordering) against the previous library; then the GPU test suite.
-set -e
-OUT=gpurun_out/order
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-mkdir -p $OUT
-LIB=$PWD/gp-mpc_amd/gpmpc/lib
+# Round-4 A/B: (a) every launch ranked by cost (GPMPC_ORDER=2: the dispatcher then deals each cost
+# quartile across the CUs) vs instance order for launches the device holds at once (configs 3, 4);
+# (b) overlapped halves on/off for the multi-round config 5.  bash tools/ab_order.sh OUTDIR
+O=${1:?outdir}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_gpu_semantics.py tests/test_gpu_parity.py tests/test_gpu_launch.py > $O/pytest.log 2>&1 || exit $?
 A="--steps 20 --warmup 5 --no-cpu-baseline"
+C4="--n-train 1000 --batch 1024"
 C5="--model quad3d --n-train 4000 --fitc 2000 --horizon 40 --batch 512 --var-inputs dynamics"
-timeout -k 10 300 python3 -u bench.py $C5 $A > $OUT/c5_order.json 2> $OUT/c5_order.err
-GPMPC_ORDER=0 timeout -k 10 300 python3 -u bench.py $C5 $A > $OUT/c5_noorder.json 2> $OUT/c5_noorder.err
-GPMPC_LIB=$LIB/libgpmpc_mi355x_head.so timeout -k 10 300 python3 -u bench.py $C5 $A > $OUT/c5_head.json 2> $OUT/c5_head.err
-for r in 1 2; do
-timeout -k 10 200 python3 -u bench.py $A > $OUT/c3_new_$r.json 2> $OUT/c3_new.err
-GPMPC_LIB=$LIB/libgpmpc_mi355x_head.so timeout -k 10 200 python3 -u bench.py $A > $OUT/c3_head_$r.json 2> $OUT/c3_head.err
+for rep in 1 2; do
+  for v in 2 1; do
+    GPMPC_ORDER=$v timeout -k 10 200 python3 -u bench.py $A >> $O/c3_o$v.jsonl 2>> $O/err || exit $?
+    GPMPC_ORDER=$v timeout -k 10 300 python3 -u bench.py $A $C4 >> $O/c4_o$v.jsonl 2>> $O/err || exit $?
+  done
+  for v in 1 0; do
+    GPMPC_OVERLAP=$v timeout -k 10 400 python3 -u bench.py --steps 10 --warmup 3 --no-cpu-baseline $C5 >> $O/c5_v$v.jsonl 2>> $O/err || exit $?
+  done
 done
-python3 - <<'PY'
-import json, glob
-for f in sorted(glob.glob("gpurun_out/order/*.json")):
-    d = json.loads([x for x in open(f) if x.startswith("{")][-1])
-    print(f.split("/")[-1], round(d["value"]), d["kernel_ms_per_step"], d["sqp_iter_mean"], d["status_counts"],
-          d["sqp_kernel_ms_per_step_distribution"]["p50"])
+python3 - $O <<'PY'
+import json, sys
+o = sys.argv[1]
+for case, vs in (("c3", ("o2", "o1")), ("c4", ("o2", "o1")), ("c5", ("v1", "v0"))):
+    for v in vs:
+        ds = [json.loads(x) for x in open(f"{o}/{case}_{v}.jsonl") if x.startswith("{")]
+        print(case, v, " ".join(
+            f"{d['ms_per_step']:.4f} ms (sqp {d['kernel_ms_per_step']['sqp']:.4f} var {d['kernel_ms_per_step']['variance']:.4f})" for d in ds),
+            "status", ds[-1]["status_counts"])
 PY
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
-tail -3 $OUT/pytest_gpu.log
