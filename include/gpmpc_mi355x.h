@@ -133,7 +133,12 @@ gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_d
  *   u0      [B][nu]  first input (return value of select_action)            (device, out)
  *   status  [B]      acados status code                                     (device, out)
  *   sqp_iter, qp_iter [B]  SQP iterations / total IPM iterations            (device, out, may be NULL)
- *   res     [B][4]   final NLP residuals stat, eq, ineq, comp               (device, out, may be NULL) */
+ *   res     [B][4]   final NLP residuals stat, eq, ineq, comp               (device, out, may be NULL)
+ * When the SQP launch needs more than one round of workgroups (more instances than the device
+ * holds at once) and the step has a variance launch, half of the step's work runs on a handle-owned
+ * side stream forked from and joined back into `stream` (results bit-identical; GPMPC_OVERLAP=0 in
+ * the environment at gpmpc_create turns it off): work queued on `stream` after the call still
+ * sees the whole step complete. */
 gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const int32_t* tstep, double* u0,
                          int32_t* status, int32_t* sqp_iter, int32_t* qp_iter, double* res, void* stream);
 
