@@ -648,12 +648,23 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     // the solves that set its length begin.  Each instance's arithmetic is unchanged (same kernels,
     // same per-instance data), so the results are bit-identical to the sequential order.
     if (var_launch && h->overlap && batch >= 2 && batch <= 16384 && sqp_overlap_ok(P, batch)) {
-        if (!h->side) {
+        if (!h->side) {   // created together or not at all
             int lo = 0, hi = 0;
             if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-            HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, lo));   // lowest priority
-            HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
+            hipStream_t side = nullptr;
+            hipEvent_t fork = nullptr, join = nullptr;
+            hipError_t ce = hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo);   // lowest priority
+            if (ce == hipSuccess) ce = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+            if (ce == hipSuccess) ce = hipEventCreateWithFlags(&join, hipEventDisableTiming);
+            if (ce != hipSuccess) {
+                if (join) (void)hipEventDestroy(join);
+                if (fork) (void)hipEventDestroy(fork);
+                if (side) (void)hipStreamDestroy(side);
+                return fail(GPMPC_ERR_HIP, std::string("side stream: ") + hipGetErrorString(ce));
+            }
+            h->side = side;
+            h->ev_fork = fork;
+            h->ev_join = join;
         }
         const int b1 = (batch + 1) / 2, b2 = batch - b1;
         HIPCHK(launch_sqp_order(S, batch, s));
@@ -680,6 +691,8 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         h->var_batch = batch;
         hipEvent_t e2 = h->profiling && mid ? take_event(h) : nullptr;
         hipError_t le = launch_sqp(P, S, io, batch, s, 0, b1);
+        // once an SQP launch is queued it will update the iterate: the host state follows it
+        if (le == hipSuccess) h->any_prev = true;
         if (le == hipSuccess) le = launch_var(b1, b2, h->order, h->side);
         if (le == hipSuccess) le = launch_sqp(P, S, io, batch, h->side, b1, b2);
         // the join is recorded whatever happened above, so the caller's stream never runs ahead of
@@ -692,7 +705,6 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             give_back(e2);
             return fail(GPMPC_ERR_HIP, std::string("launch_sqp: ") + hipGetErrorString(le));
         }
-        h->any_prev = true;
         if (mid && e2 && hipEventRecord(e2, s) == hipSuccess) {
             h->ev_sqp.push_back({mid, e2});
         } else {
