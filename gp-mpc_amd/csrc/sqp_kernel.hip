@@ -294,6 +294,9 @@ struct SqpKernel {
     // quad3d (FITC tile sums over M = 2000; phase tables of DESIGN §2.1 / §4)
     static constexpr int kCostLin = (NB + 1 > 16) ? 5 : 3;
     static constexpr int PS = NX + 1;   // row stride of P'_k = [P_k | p_k] and K'_k = [K_k | kff_k]
+    // stage stride of hq / gq: odd, so the IPM's one-stage-per-lane accesses (lanes k, k + 1, ..) hit
+    // distinct LDS banks (NB = 8 made every ds_read_b64 / ds_write_b64 of them an 8-way conflict)
+    static constexpr int NBS = NB | 1;
     static constexpr int CB = 4;        // tangent column block
     static constexpr int NCB = (NB + CB - 1) / CB;
 
@@ -345,7 +348,7 @@ struct SqpKernel {
                               + (size_t)H * NX * GS            // G'_k
                               + (size_t)H * NU * PS          // K'_k
                               + (size_t)H * NU * NU          // Ru_k^-1
-                              + (size_t)(H + 1) * NB * 2     // hq, gq
+                              + (size_t)(H + 1) * NBS * 2    // hq, gq (stage stride NBS)
                               + (size_t)(H + 1) * NX;        // dx (forward sweep; WSPL: the published residual)
         if (kMfma) {
             // closed-loop A'_k; the tightening scratch and (WSPL) the step-vector exchange Dq alias it
@@ -369,8 +372,8 @@ struct SqpKernel {
         L.G = s;   s += (size_t)H * NX * GS;
         L.K = s;   s += (size_t)H * NU * PS;
         L.Rui = s; s += (size_t)H * NU * NU;
-        L.hq = s;  s += (size_t)(H + 1) * NB;
-        L.gq = s;  s += (size_t)(H + 1) * NB;
+        L.hq = s;  s += (size_t)(H + 1) * NBS;
+        L.gq = s;  s += (size_t)(H + 1) * NBS;
         L.dxv = s; s += (size_t)(H + 1) * NX;
         L.gz = s;
         L.gc = s + (size_t)NGP * 16 * ((H + 15) / 16) * 4;
@@ -671,10 +674,10 @@ struct SqpKernel {
                 st.kc[b2] = L.K[(size_t)k * NU * PS + b2 * PS + row];
                 st.ri[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
             }
-            st.gq = L.gq[k * NB + col];
+            st.gq = L.gq[k * NBS + col];
             st.t = T[k * NX + row];
         };
-        double p = (lane < NX) ? L.gq[H * NB + lane] : 0.0;
+        double p = (lane < NX) ? L.gq[H * NBS + lane] : 0.0;
         if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
         double* pout = (lane < NX) ? L.P + (size_t)(H - 1) * PP + PO + lane : L.dummy + lane;
         const int pst = (lane < NX) ? PP : 0;
@@ -787,9 +790,9 @@ struct SqpKernel {
         for (int r = 0; r < 2; ++r) {   // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
             const int t = lr + 4 * r;
             double v = 0.0;
-            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
-            else if (t < NX && lc == CI) v = L.gq[H * NB + t];
-            else if (t == CI && lc < NX) v = L.gq[H * NB + lc];
+            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NBS + t] : 0.0;
+            else if (t < NX && lc == CI) v = L.gq[H * NBS + t];
+            else if (t == CI && lc < NX) v = L.gq[H * NBS + lc];
             pn[r] = v;
         }
         {   // P'_H (packed) for the multiplier recovery of stage H-1
@@ -826,8 +829,8 @@ struct SqpKernel {
             if (sv_t >= 0 && t == lc) { base = L.hq + sv_t; on = true; }
             else if (sv_t >= 0 && lc == CI) { base = L.gq + sv_t; on = true; }
             else if (t == CI && sv_lc >= 0) { base = L.gq + sv_lc; on = true; }
-            pd[r] = on ? base + (size_t)(H - 1) * NB : L.zero;
-            dst[r] = on ? NB : 0;
+            pd[r] = on ? base + (size_t)(H - 1) * NBS : L.zero;
+            dst[r] = on ? NBS : 0;
         }
         struct Stage { double g[2], d[3]; };
         auto load_stage = [&](Stage& st) {
@@ -961,8 +964,8 @@ struct SqpKernel {
         for (int r = 0; r < KS; ++r) {   // P'_H = [diag(hq_H[x]) | gq_H[x]]
             const int t = lr + 4 * r;
             double v = 0.0;
-            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NB + t] : 0.0;
-            else if (t < NX && lc == NX) v = L.gq[H * NB + t];
+            if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NBS + t] : 0.0;
+            else if (t < NX && lc == NX) v = L.gq[H * NBS + t];
             pn[r] = v;
         }
         {
@@ -997,13 +1000,13 @@ struct SqpKernel {
         for (int r = 0; r < KS; ++r) {
             const int t = lr + 4 * r;
             const bool dg = t < NX && t == lc, gc = t < NX && lc == NX;
-            pd11[r] = dg ? L.hq + (size_t)(H - 1) * NB + t : (gc ? L.gq + (size_t)(H - 1) * NB + t : L.zero);
-            d11st[r] = (dg || gc) ? NB : 0;
+            pd11[r] = dg ? L.hq + (size_t)(H - 1) * NBS + t : (gc ? L.gq + (size_t)(H - 1) * NBS + t : L.zero);
+            d11st[r] = (dg || gc) ? NBS : 0;
         }
         const bool g21 = lr < NU && lc == NX, d22 = lr < NU && lc == lr;
-        const double* pd21 = g21 ? L.gq + (size_t)(H - 1) * NB + NX + lr : L.zero;
-        const double* pd22 = d22 ? L.hq + (size_t)(H - 1) * NB + NX + lr : L.zero;
-        const int d21st = g21 ? NB : 0, d22st = d22 ? NB : 0;
+        const double* pd21 = g21 ? L.gq + (size_t)(H - 1) * NBS + NX + lr : L.zero;
+        const double* pd22 = d22 ? L.hq + (size_t)(H - 1) * NBS + NX + lr : L.zero;
+        const int d21st = g21 ? NBS : 0, d22st = d22 ? NBS : 0;
         struct Stage { double a[KS], b[KS], d11[KS], d21, d22; };
         auto load_stage = [&](Stage& st) {
 #pragma unroll
@@ -1270,9 +1273,9 @@ struct SqpKernel {
             const int k = e / NX, i = e - k * NX;
             const double* A = L.Acl + (size_t)k * NX * PS;
             const double* Kk = L.K + (size_t)k * NU * PS;
-            double acc = L.gq[k * NB + i];
+            double acc = L.gq[k * NBS + i];
 #pragma unroll
-            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * PS + i], L.gq[k * NB + NX + a], acc);
+            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * PS + i], L.gq[k * NBS + NX + a], acc);
 #pragma unroll
             for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
             return acc;
@@ -1294,8 +1297,8 @@ struct SqpKernel {
                                     : (ldv ? VT + (size_t)(H - 1) * NX + q.row
                                            : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0));
             const int st = lda ? NX * PS : (ldv ? NX : 0);
-            if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NB + lane];
-            double y = mfma4_vec(q, [&](int i) { return L.gq[H * NB + i]; });
+            if (lane < NX) L.P[(size_t)H * PP + PO + lane] = L.gq[H * NBS + lane];
+            double y = mfma4_vec(q, [&](int i) { return L.gq[H * NBS + i]; });
             const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
             const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
             double* out = stlo ? L.P + (size_t)(H - 1) * PP + PO + q.r
@@ -1320,7 +1323,7 @@ struct SqpKernel {
             double kf = 0.0;
 #pragma unroll
             for (int b2 = 0; b2 < NU; ++b2) {
-                double acc = L.gq[k * NB + NX + b2];
+                double acc = L.gq[k * NBS + NX + b2];
 #pragma unroll
                 for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + NX + b2], T[k * NX + l] + pn[l], acc);
                 kf = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], acc, kf);
@@ -1580,8 +1583,8 @@ struct SqpKernel {
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
             const int v = vb + j < NB ? vb + j : NB - 1;   // (slots past NB: inactive, any finite value)
-            blo[j] = L.hq[(size_t)kk * NB + v];
-            bup[j] = L.gq[(size_t)kk * NB + v];
+            blo[j] = L.hq[(size_t)kk * NBS + v];
+            bup[j] = L.gq[(size_t)kk * NBS + v];
             gv[j] = L.Dq[(size_t)kk * NB + v];
             hd[j] = hdiag(P, v, lane, H);
             d[j] = (lane == 0 && v < NX) ? L.xs[4 * NWAVES + (v < NX ? v : 0)] : 0.0;
@@ -1670,8 +1673,8 @@ struct SqpKernel {
                         // Riccati data: hq = H + Sigma; predictor gq with r_ml = ll sl, r_mu = lu su
                         const double hv = hd[j] + (av ? ll[j] * isl[j] + lu[j] * isu[j] : 0.0);
                         const double gqv = av ? rd + ll[j] + ll[j] * rl * isl[j] - lu[j] - lu[j] * ru * isu[j] : 0.0;
-                        L.hq[k_q * NB + vb + j] = hv;
-                        L.gq[k_q * NB + vb + j] = gqv;
+                        L.hq[k_q * NBS + vb + j] = hv;
+                        L.gq[k_q * NBS + vb + j] = gqv;
                     }
                 }
 #pragma unroll
@@ -1760,7 +1763,7 @@ struct SqpKernel {
                         const double dsl = dd[j] + rl, dsu = -dd[j] + ru;
                         const double dll = -ll[j] * fma(dsl, isl[j], 1.0);
                         const double dlu = -lu[j] * fma(dsu, isu[j], 1.0);
-                        L.gq[k_q * NB + vb + j] += (dll * dsl - smu) * isl[j] - (dlu * dsu - smu) * isu[j];
+                        L.gq[k_q * NBS + vb + j] += (dll * dsl - smu) * isl[j] - (dlu * dsu - smu) * isu[j];
                     }
                 }
                 XSYNC();
@@ -2159,8 +2162,8 @@ struct SqpKernel {
                 if (on) {
 #pragma unroll
                     for (int v = 0; v < NB; ++v) {
-                        L.hq[(size_t)k * NB + v] = lbv(v) - w[v];
-                        L.gq[(size_t)k * NB + v] = ubv(v) - w[v];
+                        L.hq[(size_t)k * NBS + v] = lbv(v) - w[v];
+                        L.gq[(size_t)k * NBS + v] = ubv(v) - w[v];
                         L.Dq[(size_t)k * NB + v] = g[v];
                     }
 #pragma unroll
