@@ -24,13 +24,14 @@ __device__ void init_stage_data(const typename SqpKernel<ID>::Lds& L, int H, int
     if (lane < 8) L.zero[lane] = (lane == 7) ? 1.0 : 0.0;
     // synthetic, well-conditioned stage data: G' = [I + 0.01 R | 0.1 R | c], hq >= 1
     for (int e = lane; e < H * NX * GS; e += 64) {
-        const int j = e % GS, i = (e / GS) % NX;
+        const int j = e % GS, i = (e / GS) % NX, k = e / (NX * GS);
         const double r = 0.5 - 0.37 * ((e * (7919 + salt)) % 101) / 101.0;
-        L.G[e] = (j < NX) ? ((i == j) ? 1.0 : 0.0) + 0.01 * r : (j < NB ? 0.1 * r : 0.01 + 0.02 * r);
+        L.G[(size_t)k * NX * GS + i * GS + j] = (j < NX) ? ((i == j) ? 1.0 : 0.0) + 0.01 * r : (j < NB ? 0.1 * r : 0.01 + 0.02 * r);
     }
     for (int e = lane; e < (H + 1) * NB; e += 64) {
-        L.hq[e] = 1.0 + 0.1 * ((e * (31 + salt)) % 17);
-        L.gq[e] = 0.01 * ((e * (13 + salt)) % 7) - 0.03;
+        const int kk = e / NB, v = e - kk * NB;
+        L.hq[kk * K::NBS + v] = 1.0 + 0.1 * ((e * (31 + salt)) % 17);
+        L.gq[kk * K::NBS + v] = 0.01 * ((e * (13 + salt)) % 7) - 0.03;
     }
     __syncthreads();
     K::mfma_backward_h(L, H, lane);
