@@ -670,14 +670,16 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
         // cartpole 256: 10.1 -> 9.0 us; at 512 and 1024 instances the split is slower: 38 -> 42 / 51 us,
         // 71 -> 77 us; two waves per point tile measured between the two, eight: 128 instances 19 us,
         // 256: 33 us, ab_varsplit8/).  GPMPC_VAR_SPLIT=1/4 forces a choice (A/B runs).
-        static int ncu = 0, force = -1;
-        if (ncu == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-                ncu = 256;
+        static const int ncu = [] {   // (thread-safe one-time initialisation)
+            int dev = 0, n = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+                n = 256;
+            return n;
+        }();
+        static const int force = [] {
             const char* f = std::getenv("GPMPC_VAR_SPLIT");
-            force = f ? std::atoi(f) : -1;
-        }
+            return f ? std::atoi(f) : -1;
+        }();
         const int step_blocks = pb.step_points > 0 ? (pb.step_points + 16 * kPostWaves - 1) / (16 * kPostWaves) : blocks;
         const int wgs = step_blocks * pb.n;   // the split choice follows the whole step (bit-identical halves)
         int split = 2 * wgs <= ncu ? 4 : 1;
