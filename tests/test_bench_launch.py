@@ -132,3 +132,28 @@ def test_flop_counts_match_survey_8d():
     assert bench.survey_flops_per_lin(spec, N, H) == H * 4 * N * (thrust + pitch) == 480_000
     assert exps_lin == H * N * (1 + 4)
     assert var == 2 * H * (N * (N + 1) + 2 * N)
+
+
+def test_shard_mode_runs_one_rank_alone():
+    """--shard R/N measures one rank of an N-rank strong-scaled job by itself (tools/shard_sweep.sh):
+    it is a single process on the GPU, so it refuses a process group and the CPU rehearsal."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--shard", "1/2", "--dry-run", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=240, cwd=str(ROOT))
+    assert p.returncode != 0 and "--shard R/N runs one rank alone" in p.stderr
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--shard", "2/2", "--steps", "1"],
+                       capture_output=True, text=True, env=env, timeout=240, cwd=str(ROOT))
+    assert p.returncode != 0 and "0 <= R < N" in p.stderr
+
+
+@pytest.mark.gpu
+def test_emulated_shard_line_on_the_gpu():
+    """Every rank's shard reports its own line (rank > 0 included): its slice of the metric's global
+    batch, value = the shard's instances x steps / its time, no CPU baseline."""
+    out = _gpu_bench(["--shard", "3/8", "--steps", "2", "--warmup", "1"])
+    assert out["emulated_shard"]["rank"] == 3 and out["emulated_shard"]["world"] == 8
+    assert out["emulated_shard"]["instances"] == [384, 512] and out["config"]["batch_per_gpu"] == 128
+    assert out["cpu_baseline"] is None and out["scaling"] == "strong"
+    assert abs(out["value"] - 128 * 2 / (out["ms_per_step"] * 2e-3)) <= 1e-6 * out["value"]
+    assert sum(out["status_counts"].values()) == 128 * 2
