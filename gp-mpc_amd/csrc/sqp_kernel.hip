@@ -596,7 +596,7 @@ struct SqpKernel {
             for (int j = 0; j < PS; ++j) st.kr[j] = kp[(size_t)k * NU * PS + j];
         };
         if (lane < NX) L.dxv[lane] = 0.0;
-        double* out = (lane < NX) ? L.dxv + NX + lane : L.dummy + lane;
+        double* out = (lane < NX) ? L.dxv + NX + lane : L.dummy;
         const int ost = (lane < NX) ? NX : 0;
         double x = 0.0;
         auto step = [&](const St& st) {
@@ -679,9 +679,9 @@ struct SqpKernel {
         };
         double p = (lane < NX) ? L.gq[H * NBS + lane] : 0.0;
         if (lane < NX) L.P[(size_t)H * PP + PO + lane] = p;
-        double* pout = (lane < NX) ? L.P + (size_t)(H - 1) * PP + PO + lane : L.dummy + lane;
+        double* pout = (lane < NX) ? L.P + (size_t)(H - 1) * PP + PO + lane : L.dummy;
         const int pst = (lane < NX) ? PP : 0;
-        double* kout = (lane >= NX && lane < NB) ? L.K + (size_t)(H - 1) * NU * PS + a * PS + NX : L.dummy + lane;
+        double* kout = (lane >= NX && lane < NB) ? L.K + (size_t)(H - 1) * NU * PS + a * PS + NX : L.dummy;
         const int kst = (lane >= NX && lane < NB) ? NU * PS : 0;
         auto step = [&](int k, const St& st) {
             const double pv = st.t + p;
@@ -853,14 +853,14 @@ struct SqpKernel {
             const int t = lr + 4 * r;
             const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc));
             const int idx = (lc == CI) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
-            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy + lane;
+            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy;
             sp_st[r] = st ? PP : 0;
         }
         const bool kst = lr < NU && (lc < NX || lc == CI);
-        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + (lc == CI ? NX : lc) : L.dummy + lane;
+        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + (lc == CI ? NX : lc) : L.dummy;
         const int sk_st = kst ? NU * PS : 0;
         const bool rst = lane < NU * NU;
-        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lane : L.dummy + lane;
+        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lane : L.dummy;
         const int srui_st = rst ? NU * NU : 0;
         double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
         bool pend = false;
@@ -1031,14 +1031,14 @@ struct SqpKernel {
             const int t = lr + 4 * r;
             const bool st = t < NX && ((lc == NX) || (lc < NX && t <= lc));
             const int idx = (lc == NX) ? PO + t : pidx(t < lc ? t : lc, t < lc ? lc : t);
-            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy + lane;
+            sp[r] = st ? L.P + (size_t)(H - 1) * PP + idx : L.dummy;
             sp_st[r] = st ? PP : 0;
         }
         const bool kst = lr < NU && lc <= NX;
-        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + lc : L.dummy + lane;
+        double* sk = kst ? L.K + (size_t)(H - 1) * NU * PS + lr * PS + lc : L.dummy;
         const int sk_st = kst ? NU * PS : 0;
         const bool rst = lr < NU && lc < NU;
-        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lr * NU + lc : L.dummy + lane;
+        double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lr * NU + lc : L.dummy;
         const int srui_st = rst ? NU * NU : 0;
         const unsigned ma0 = lr == 0 ? ~0u : 0u, ma1 = lr == 1 ? ~0u : 0u, ma2 = lr == 2 ? ~0u : 0u;
         const unsigned mb1 = (lr & 2) ? ~0u : 0u, mb2 = (lr & 1) ? ~0u : 0u, mb3 = ((lr ^ (lr >> 1)) & 1) ? ~0u : 0u;
@@ -1223,7 +1223,7 @@ struct SqpKernel {
             const int st = ld ? NX * PS : 0;
             const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
             const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
-            double* out = stlo ? L.dxv + NX + q.r : (sthi ? L.dxv + NX + 4 + q.r : L.dummy + lane);
+            double* out = stlo ? L.dxv + NX + q.r : (sthi ? L.dxv + NX + 4 + q.r : L.dummy);
             const int ost = (stlo || sthi) ? NX : 0;
             if (lane < NX) L.dxv[lane] = 0.0;
             double y = mfma4_vec(q, [](int) { return 0.0; });
@@ -1302,7 +1302,7 @@ struct SqpKernel {
             const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
             const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
             double* out = stlo ? L.P + (size_t)(H - 1) * PP + PO + q.r
-                               : (sthi ? L.P + (size_t)(H - 1) * PP + PO + 4 + q.r : L.dummy + lane);
+                               : (sthi ? L.P + (size_t)(H - 1) * PP + PO + 4 + q.r : L.dummy);
             const int ost = (stlo || sthi) ? PP : 0;
             double an = *src;
             for (int k = H - 1; k >= 0; --k) {
