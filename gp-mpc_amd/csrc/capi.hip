@@ -67,7 +67,7 @@ struct gpmpc_handle {
     int32_t* has_prev = nullptr;
     double* lin = nullptr;          // linearisation cache of the stored iterate (StateDev::lin)
     int32_t* lin_tag = nullptr;
-    bool lin_cache = true;
+    bool lin_cache = true;          // GPMPC_TUNE_LIN_CACHE
     int32_t* order = nullptr;       // cost-ordered dispatch (StateDev::order / cost)
     uint32_t* cost = nullptr;
     double* traj = nullptr;
@@ -99,29 +99,53 @@ struct gpmpc_handle {
     // the batch whose tightening variances the last solve's variance launch wrote into `var`
     // (0: the last solve ran none, var is stale or unset)
     int var_batch = 0;
-    // stream of the last call that queued work on the handle's device state; a call on another
-    // stream first waits for it (order_after_last), so consecutive calls never overlap
+    // stream of the last call that queued work on the handle's device state and an event recorded
+    // on it when that call returned: a call on another stream first waits for the event
+    // (order_after_last / StreamMark), so consecutive calls never overlap
     hipStream_t last_stream = nullptr;
-    bool last_stream_valid = false;
+    hipEvent_t ev_last = nullptr;
+    bool ev_last_valid = false;
     // overlapped steps (gpmpc_solve): the second half's variance and SQP launches run on `side`,
     // forked from and joined back into the caller's stream by two events
-    bool overlap = true;
+    bool overlap = true;            // GPMPC_TUNE_OVERLAP
+    int var_split = 0;              // GPMPC_TUNE_VAR_SPLIT
+    bool event_fence = false;       // GPMPC_TUNE_EVENT_FENCE
+    double* stage_cost = nullptr;   // caller's [max_batch][H+1] stage-cost buffer (StepIO::stage_cost)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
 
 // The handle's device state (iterate, multipliers, variances, dispatch order) is read and written
-// by every queued call, so calls on different streams must not overlap: when the stream changes,
-// the new call waits for the previous stream's work (host synchronisation, only on a change).
+// by every queued call, so calls on different streams must not overlap.  Each such call ends by
+// recording the handle's event on its stream (StreamMark); a call on another stream first makes
+// its stream wait for that event.  No host synchronisation, and a destroyed previous stream leaves
+// nothing dangling (the event outlives it).
 static hipError_t order_after_last(gpmpc_handle* h, hipStream_t s) {
-    if (h->last_stream_valid && h->last_stream != s) {
-        const hipError_t e = hipStreamSynchronize(h->last_stream);
-        if (e != hipSuccess) return e;
+    if (!h->ev_last) {
+        const hipError_t e = hipEventCreateWithFlags(&h->ev_last, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            h->ev_last = nullptr;
+            return e;
+        }
     }
-    h->last_stream = s;
-    h->last_stream_valid = true;
+    if (h->ev_last_valid && h->last_stream != s) return hipStreamWaitEvent(s, h->ev_last, 0);
     return hipSuccess;
 }
+// Records the handle's event on the call's stream when the call returns, whatever it queued.  If
+// the record fails the stream is drained on the host instead, so the next call needs no wait.
+struct StreamMark {
+    gpmpc_handle* h;
+    hipStream_t s;
+    ~StreamMark() {
+        if (h->ev_last && hipEventRecord(h->ev_last, s) == hipSuccess) {
+            h->ev_last_valid = true;
+        } else {
+            (void)hipStreamSynchronize(s);
+            h->ev_last_valid = false;
+        }
+        h->last_stream = s;
+    }
+};
 
 static hipEvent_t take_event(gpmpc_handle* h) {
     if (!h->ev_pool.empty()) {
@@ -132,8 +156,7 @@ static hipEvent_t take_event(gpmpc_handle* h) {
     hipEvent_t e = nullptr;
     // timing-only events: no system-scope fence (cache writeback / invalidate) when recorded,
     // which otherwise adds ~5 us of dispatch gap around every kernel it brackets
-    const char* ev = std::getenv("GPMPC_EVENT_FENCE");   // "1": default (fenced) events, for A/B
-    const unsigned flags = (ev && ev[0] == '1') ? hipEventDefault : hipEventDisableSystemFence;
+    const unsigned flags = h->event_fence ? hipEventDefault : hipEventDisableSystemFence;
     if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
     return e;
 }
@@ -153,6 +176,7 @@ static void free_handle(gpmpc_handle* h) {
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->ev_last) (void)hipEventDestroy(h->ev_last);
     if (h->side) (void)hipStreamDestroy(h->side);
     for (double* p : {h->x, h->u, h->pi, h->lam, h->var, h->tight, h->traj, h->plant_params, h->tgain, h->lin})
         if (p) (void)hipFree(p);
@@ -243,17 +267,9 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.qp_tol = 1e-6;
     P.qp_mu0 = 1.0;
     P.lin_gen = 1;   // tags start at 0: nothing cached
+    P.waves = 0;            // automatic launch shape (gpmpc_set_launch)
+    P.order_dispatch = 1;   // cost-ordered dispatch of multi-round launches (GPMPC_TUNE_ORDER)
     {
-        const char* ev = std::getenv("GPMPC_LIN_CACHE");   // "0": recompute every linearisation (A/B)
-        h->lin_cache = !(ev && ev[0] == '0');
-        const char* ew = std::getenv("GPMPC_WAVES");       // "1" / "2" / "4": waves per instance (A/B)
-        P.waves = ew ? std::atoi(ew) : 0;
-        if (P.waves != 1 && P.waves != 2 && P.waves != 4) P.waves = 0;
-        if (model_id == kQuad3D) P.waves = 0;             // quad3d always runs its four waves
-        const char* eo = std::getenv("GPMPC_ORDER");       // "0": instance order, "2": rank every launch (A/B)
-        P.order_dispatch = (eo && eo[0] == '0') ? 0 : ((eo && eo[0] == '2') ? 2 : 1);
-        const char* ov = std::getenv("GPMPC_OVERLAP");     // "0": one variance launch, then one SQP launch (A/B)
-        h->overlap = !(ov && ov[0] == '0');
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
         P.n_cu = ncu;
@@ -548,6 +564,7 @@ gpmpc_status gpmpc_reset(gpmpc_handle* h, int32_t batch, int32_t reset_iterate, 
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
     HIPCHK(order_after_last(h, s));
+    StreamMark mark{h, s};
     HIPCHK(hipMemsetAsync(h->has_prev, 0, B * sizeof(int32_t), s));
     bump_lin(h);
     if (reset_iterate) {
@@ -568,6 +585,7 @@ gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_d
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
     HIPCHK(order_after_last(h, s));
+    StreamMark mark{h, s};
     HIPCHK(hipMemcpyAsync(h->x, x_dev, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
     HIPCHK(hipMemcpyAsync(h->u, u_dev, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
     bump_lin(h);
@@ -589,6 +607,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(order_after_last(h, s));
+    StreamMark mark{h, s};
     ProblemDev P = h->P;
     P.tighten = (h->P.tighten && h->P.use_gp) ? 1 : 0;
     // Profiling events are best effort: a failed record drops that launch's timing (the events go
@@ -603,6 +622,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         PostBatch pb{};
         pb.n = h->md.ngp;
         pb.step_points = batch * h->H;
+        pb.var_split = h->var_split;
         for (int g = 0; g < h->md.ngp; ++g) {
             PostArgs& a = pb.a[g];
             a.sx = h->x;
@@ -688,12 +708,16 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             if (mid) h->ev_var_owned.push_back(mid);
             return fail(GPMPC_ERR_HIP, std::string("variance launch: ") + hipGetErrorString(ve));
         }
-        h->var_batch = batch;
+        // var rows are valid only for what is queued: the costlier half now (ranked instances, so
+        // no prefix of the batch is complete: none), the whole batch once the second half's
+        // variance launch is queued too
+        h->var_batch = 0;
         hipEvent_t e2 = h->profiling && mid ? take_event(h) : nullptr;
         hipError_t le = launch_sqp(P, S, io, batch, s, 0, b1);
         // once an SQP launch is queued it will update the iterate: the host state follows it
         if (le == hipSuccess) h->any_prev = true;
         if (le == hipSuccess) le = launch_var(b1, b2, h->order, h->side);
+        if (le == hipSuccess) h->var_batch = batch;
         if (le == hipSuccess) le = launch_sqp(P, S, io, batch, h->side, b1, b2);
         // the join is recorded whatever happened above, so the caller's stream never runs ahead of
         // work already queued on the side stream
@@ -711,6 +735,7 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
             if (mid) h->ev_var_owned.push_back(mid);
             give_back(e2);
         }
+        if (h->stage_cost) HIPCHK(launch_stage_cost(P, h->x, h->u, tstep, status, h->stage_cost, batch, s));
         return GPMPC_OK;
     }
 
@@ -764,6 +789,8 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     h->any_prev = true;
     if (e0 && e1 && hipEventRecord(e1, s) == hipSuccess) h->ev_sqp.push_back({e0, e1});
     else recycle();   // lost profiling data only
+    // stage costs of the stored solution, behind the SQP launch (and outside its timing events)
+    if (h->stage_cost) HIPCHK(launch_stage_cost(P, h->x, h->u, tstep, status, h->stage_cost, batch, s));
     return GPMPC_OK;
 }
 
@@ -777,6 +804,7 @@ gpmpc_status gpmpc_get_variance(gpmpc_handle* h, int32_t batch, double* var_dev,
     (void)hipSetDevice(h->device);
     hipStream_t s = (hipStream_t)stream;
     HIPCHK(order_after_last(h, s));
+    StreamMark mark{h, s};
     const size_t B = batch, H = h->H;
     HIPCHK(hipMemcpyAsync(var_dev, h->var, B * H * h->md.ngp * sizeof(double), hipMemcpyDeviceToDevice, s));
     return GPMPC_OK;
@@ -788,6 +816,57 @@ gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves) {
     if (h->model == kQuad3D && waves != 0 && waves != 4)
         return fail(GPMPC_ERR_ARG, "quad3d runs four waves per instance (waves must be 0 or 4)");
     h->P.waves = waves;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* waves, int32_t* overlapped) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    if (waves) *waves = sqp_launch_waves(h->P, batch);
+    // the overlap needs a variance launch (tightening with GPs) besides the shape
+    if (overlapped)
+        *overlapped = (h->overlap && h->P.tighten && h->P.use_gp && batch >= 2 && batch <= 16384 &&
+                       sqp_overlap_ok(h->P, batch)) ? 1 : 0;
+    return GPMPC_OK;
+}
+
+gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    switch (option) {
+        case GPMPC_TUNE_LIN_CACHE:
+            if (value != 0 && value != 1) break;
+            if (h->lin_cache != (value == 1)) bump_lin(h);   // tags written under the other setting are stale
+            h->lin_cache = value == 1;
+            return GPMPC_OK;
+        case GPMPC_TUNE_ORDER:
+            if (value < 0 || value > 2) break;
+            h->P.order_dispatch = value;
+            return GPMPC_OK;
+        case GPMPC_TUNE_OVERLAP:
+            if (value != 0 && value != 1) break;
+            h->overlap = value == 1;
+            return GPMPC_OK;
+        case GPMPC_TUNE_VAR_SPLIT:
+            if (value != 0 && value != 1 && value != 4) break;
+            h->var_split = value;
+            return GPMPC_OK;
+        case GPMPC_TUNE_EVENT_FENCE:
+            if (value != 0 && value != 1) break;
+            if (h->event_fence != (value == 1)) {   // pooled events carry the old flags
+                for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+                h->ev_pool.clear();
+            }
+            h->event_fence = value == 1;
+            return GPMPC_OK;
+        default:
+            return fail(GPMPC_ERR_ARG, "unknown tuning option " + std::to_string(option));
+    }
+    return fail(GPMPC_ERR_ARG, "bad value " + std::to_string(value) + " for tuning option " + std::to_string(option));
+}
+
+gpmpc_status gpmpc_set_cost_buffer(gpmpc_handle* h, void* cost_dev) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    h->stage_cost = (double*)cost_dev;
     return GPMPC_OK;
 }
 
@@ -884,6 +963,7 @@ gpmpc_status gpmpc_get_solution(gpmpc_handle* h, int32_t batch, double* x_dev, d
     hipStream_t s = (hipStream_t)stream;
     const size_t B = batch, H = h->H;
     HIPCHK(order_after_last(h, s));
+    StreamMark mark{h, s};
     if (x_dev) HIPCHK(hipMemcpyAsync(x_dev, h->x, B * (H + 1) * h->md.nx * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (u_dev) HIPCHK(hipMemcpyAsync(u_dev, h->u, B * H * h->md.nu * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (tight_dev)

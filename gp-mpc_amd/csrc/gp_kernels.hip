@@ -14,7 +14,7 @@
 #include "models.h"
 
 #include <algorithm>
-#include <cstdlib>
+#include <atomic>
 #include <type_traits>
 
 namespace gpmpc {
@@ -669,33 +669,32 @@ hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_
         // (measured, profiles/r4/ab_varsplit/: 128 quad2d instances 35.9 -> 19.7 us, 256: 36.5 -> 28.5 us,
         // cartpole 256: 10.1 -> 9.0 us; at 512 and 1024 instances the split is slower: 38 -> 42 / 51 us,
         // 71 -> 77 us; two waves per point tile measured between the two, eight: 128 instances 19 us,
-        // 256: 33 us, ab_varsplit8/).  GPMPC_VAR_SPLIT=1/4 forces a choice (A/B runs).
+        // 256: 33 us, ab_varsplit8/).  PostBatch::var_split = 1 / 4 forces a choice (GPMPC_TUNE_VAR_SPLIT).
         static const int ncu = [] {   // (thread-safe one-time initialisation)
             int dev = 0, n = 0;
             if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
                 n = 256;
             return n;
         }();
-        static const int force = [] {
-            const char* f = std::getenv("GPMPC_VAR_SPLIT");
-            return f ? std::atoi(f) : -1;
-        }();
         const int step_blocks = pb.step_points > 0 ? (pb.step_points + 16 * kPostWaves - 1) / (16 * kPostWaves) : blocks;
         const int wgs = step_blocks * pb.n;   // the split choice follows the whole step (bit-identical halves)
         int split = 2 * wgs <= ncu ? 4 : 1;
-        if (force == 1 || force == 4) split = force;
+        if (pb.var_split == 1 || pb.var_split == 4) split = pb.var_split;
         return from_state ? launch_var_tri<true>(pb, pb.npad[0] / 16, blocks, split, stream)
                           : launch_var_tri<false>(pb, pb.npad[0] / 16, blocks, split, stream);
     }
-    static bool attr = false;
-    if (!attr) {
+    // dynamic-LDS limit of the post kernels, raised once per process; the latch is atomic because
+    // handles on different host threads may launch concurrently (a race sets the same attribute
+    // twice, which is harmless), and it stays clear when a call fails so the next launch retries
+    static std::atomic<bool> attr{false};
+    if (!attr.load(std::memory_order_acquire)) {
         const int mx = 2 * 16 * post_stride(kMaxCT) * (int)sizeof(double);
         for (const void* k : {(const void*)gp_post_kernel<true, false>, (const void*)gp_post_kernel<false, false>,
                               (const void*)gp_post_kernel<true, true>, (const void*)gp_post_kernel<false, true>}) {
             const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
             if (e != hipSuccess) return e;
         }
-        attr = true;
+        attr.store(true, std::memory_order_release);
     }
     bool full = true;   // every variance entry's column groups have kMaxCT tiles
     for (int q = 0; q < pb.n; ++q) {

@@ -83,7 +83,7 @@ struct ProblemDev {
     int32_t waves;
     int32_t n_cu;             // compute units of the device (set by gpmpc_create)
     // cost-ordered dispatch (StateDev::order): on when a launch has more instances than the
-    // device holds at once (GPMPC_ORDER=0 turns it off, =2 ranks every launch, for A/B)
+    // device holds at once (gpmpc_set_tuning GPMPC_TUNE_ORDER: 0 off, 2 ranks every launch)
     int32_t order_dispatch;
     GPDev gp[kMaxGP];
 };
@@ -231,6 +231,8 @@ struct PostBatch {
     // points of the whole step when this launch is one part of it (the overlapped halves): the
     // kernel choice follows the step, so both halves use the kernel a single launch would (0: P)
     int32_t step_points;
+    // triangular variance kernel's column split (GPMPC_TUNE_VAR_SPLIT): 0 automatic, 1 or 4 forced
+    int32_t var_split;
 };
 
 // Launchers (sqp_kernel.hip, gp_kernels.hip).
@@ -239,8 +241,11 @@ hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, 
                       int first = 0, int count = -1);
 hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream);
 bool sqp_overlap_ok(const ProblemDev& P, int batch);
+int sqp_launch_waves(const ProblemDev& P, int batch);   // waves per instance launch_sqp would use
 size_t sqp_lds_bytes(int model, int H);
 int model_unc_dims(int model, int32_t* unc);   // the model's uncertain state dims (Bd columns), returns their count
+hipError_t launch_stage_cost(const ProblemDev& P, const double* x, const double* u, const int32_t* tstep,
+                             const int32_t* status, double* cost, int B, hipStream_t stream);
 hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* mean, double* grad, hipStream_t stream);
 hipError_t launch_gp_post(const GPDev& g, int npad, const PostArgs& a, bool from_state, hipStream_t stream);
 hipError_t launch_gp_post_batch(const PostBatch& pb, bool from_state, hipStream_t stream);

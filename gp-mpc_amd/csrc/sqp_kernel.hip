@@ -22,7 +22,6 @@
 // split over lanes k and k + 32 when H + 1 <= 32 (SPL).  The Riccati recursion is sequential
 // over stages and parallel over matrix entries.  DESIGN.md §2.1 has the layouts and timings.
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "gpmpc_common.h"
@@ -2347,6 +2346,53 @@ hipError_t launch_gp_mean_grad(const GPDev& g, const double* Z, int P, double* m
     return hipGetLastError();
 }
 
+// LINEAR_LS stage costs of the stored solution (gpmpc_set_cost_buffer), one thread per (instance,
+// stage), queued right behind the SQP launch: cost[b][k] = 1/2 ||y_k - y_ref,k||^2_W, y = [x; u],
+// W = dt blkdiag(Q, R) on stages 0..H-1 and Q on stage H (gpmpc.py:231-239, mpc.py:101-102, acados
+// cost_scaling); NaN for an instance whose solve failed (status 1 / 4: x, u hold the previous
+// solution).  A separate kernel so that the SQP kernel's register allocation does not change.
+template <int ID>
+__global__ __launch_bounds__(256) void stage_cost_kernel(ProblemDev P, const double* __restrict__ x,
+                                                         const double* __restrict__ u, const int32_t* __restrict__ tstep,
+                                                         const int32_t* __restrict__ status, double* __restrict__ cost,
+                                                         int B) {
+    using M = Model<ID>;
+    constexpr int NX = M::NX, NU = M::NU;
+    const int H = P.H;
+    const int e = blockIdx.x * 256 + threadIdx.x;
+    if (e >= B * (H + 1)) return;
+    const int b = e / (H + 1), k = e - b * (H + 1);
+    const int tref = (tstep[b] + k) % P.traj_len;
+    const double ws = k < H ? P.cost_scale : 1.0;
+    double c = 0.0;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        const double d = x[((size_t)b * (H + 1) + k) * NX + i] - P.traj[(size_t)tref * NX + i];
+        c = fma(0.5 * ws * P.q[i] * d, d, c);
+    }
+    if (k < H) {
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            const double d = u[((size_t)b * H + k) * NU + a] - P.u_eq[a];
+            c = fma(0.5 * P.cost_scale * P.r[a] * d, d, c);
+        }
+    }
+    const int st = status[b];
+    cost[e] = (st == kSuccess || st == kMaxIter) ? c : __builtin_nan("");
+}
+
+hipError_t launch_stage_cost(const ProblemDev& P, const double* x, const double* u, const int32_t* tstep,
+                             const int32_t* status, double* cost, int B, hipStream_t stream) {
+    const int n = B * (P.H + 1), blocks = (n + 255) / 256;
+    switch (P.model) {
+        case kQuad2D: hipLaunchKernelGGL(stage_cost_kernel<kQuad2D>, dim3(blocks), dim3(256), 0, stream, P, x, u, tstep, status, cost, B); break;
+        case kQuad3D: hipLaunchKernelGGL(stage_cost_kernel<kQuad3D>, dim3(blocks), dim3(256), 0, stream, P, x, u, tstep, status, cost, B); break;
+        case kCartpole: hipLaunchKernelGGL(stage_cost_kernel<kCartpole>, dim3(blocks), dim3(256), 0, stream, P, x, u, tstep, status, cost, B); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 // order[r] = the instance of rank r by decreasing cost (ties by instance id: a permutation);
 // one thread per instance counts the instances ranked before it.  Used only for multi-round
 // launches (a few hundred to a few thousand instances: O(B^2 / threads) broadcast LDS reads).
@@ -2471,6 +2517,14 @@ bool sqp_overlap_ok(const ProblemDev& P, int batch) {
         case kCartpole: return overlap_ok_of<kCartpole>(P, batch);
     }
     return false;
+}
+int sqp_launch_waves(const ProblemDev& P, int batch) {
+    switch (P.model) {
+        case kQuad2D: return sqp_waves<kQuad2D>(P, batch);
+        case kQuad3D: return sqp_waves<kQuad3D>(P, batch);
+        case kCartpole: return sqp_waves<kCartpole>(P, batch);
+    }
+    return 0;
 }
 
 // order[] = the instances by decreasing cost of their last solve

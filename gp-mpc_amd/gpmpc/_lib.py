@@ -51,7 +51,13 @@ SIGNATURES = {
     "gpmpc_set_stats_buffer": (_I, [_P, _P, _I]),
     "gpmpc_get_variance": (_I, [_P, _I, _P, _P]),
     "gpmpc_lds_bytes": (c_int64, [_I, _I]),
+    "gpmpc_get_launch_info": (_I, [_P, _I, POINTER(_I), POINTER(_I)]),
+    "gpmpc_set_tuning": (_I, [_P, _I, _I]),
+    "gpmpc_set_cost_buffer": (_I, [_P, _P]),
 }
+
+# gpmpc_set_tuning options (include/gpmpc_mi355x.h GPMPC_TUNE_*)
+TUNE = {"lin_cache": 0, "order": 1, "overlap": 2, "var_split": 3, "event_fence": 4}
 
 
 class GPMPCError(RuntimeError):

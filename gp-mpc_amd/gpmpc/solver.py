@@ -202,6 +202,32 @@ class BatchSolver:
         0 or 4).  A performance option; results agree to rounding."""
         _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves)))
 
+    def launch_info(self) -> dict:
+        """What a solve of this batch runs (gpmpc_get_launch_info): SQP waves per instance, and
+        whether a step with a variance launch runs as overlapped halves (then the profiling events
+        bracket spans of the step, not single kernels)."""
+        w, o = ctypes.c_int32(), ctypes.c_int32()
+        _lib.check(self.lib.gpmpc_get_launch_info(self._h, self.batch, ctypes.byref(w), ctypes.byref(o)))
+        return {"waves": w.value, "overlapped": bool(o.value)}
+
+    def set_tuning(self, **opts):
+        """Performance switches (gpmpc_set_tuning): lin_cache=0/1, order=0/1/2, overlap=0/1,
+        var_split=0/1/4, event_fence=0/1.  Outputs do not depend on them (A/B knobs)."""
+        for k, v in opts.items():
+            if k not in _lib.TUNE:
+                raise ValueError(f"unknown tuning option {k!r} (one of {sorted(_lib.TUNE)})")
+            _lib.check(self.lib.gpmpc_set_tuning(self._h, _lib.TUNE[k], int(v)))
+
+    def set_cost_output(self, enabled: bool = True) -> torch.Tensor | None:
+        """Per-stage LINEAR_LS costs of every solve's new solution into ``self.stage_cost`` (B, H+1)
+        (gpmpc_set_cost_buffer): 1/2 ||y_k - y_ref,k||^2_W with dt-scaled stage weights and the
+        unscaled terminal weight (`gpmpc/gpmpc.py:231-239`); NaN for a failed solve."""
+        self.stage_cost = (torch.full((self.batch, self.H + 1), float("nan"), dtype=torch.float64, device=self.device)
+                           if enabled else None)
+        _lib.check(self.lib.gpmpc_set_cost_buffer(self._h, None if self.stage_cost is None
+                                                  else self.stage_cost.data_ptr()))
+        return self.stage_cost
+
     def set_profiling(self, enabled: bool):
         _lib.check(self.lib.gpmpc_set_profiling(self._h, int(enabled)))
 

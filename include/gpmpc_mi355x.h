@@ -10,9 +10,10 @@
  * Threading: one handle per GPU/process, driven by one host thread at a time
  * (the reference drives one acados solver from one Python thread, gpmpc/gpmpc.py:105-107).
  * Streams: every call queues its work on its stream argument.  The handle's device state is
- * shared by all of them, so when a call names a different stream than the previous call, the
- * handle first waits on the host for the previous stream's work; use one stream per handle
- * (what BatchSolver does) to keep every call asynchronous.
+ * shared by all of them, so each call that touches it ends by recording a handle-owned event on
+ * its stream, and a call on a different stream first makes its stream wait for that event
+ * (hipStreamWaitEvent: no host synchronisation, and the previous stream may already be gone).
+ * The library reads no environment variables: every option is an explicit call.
  */
 #ifndef GPMPC_MI355X_H
 #define GPMPC_MI355X_H
@@ -136,9 +137,9 @@ gpmpc_status gpmpc_set_iterate(gpmpc_handle* h, int32_t batch, const double* x_d
  *   res     [B][4]   final NLP residuals stat, eq, ineq, comp               (device, out, may be NULL)
  * When the SQP launch needs more than one round of workgroups (more instances than the device
  * holds at once) and the step has a variance launch, half of the step's work runs on a handle-owned
- * side stream forked from and joined back into `stream` (results bit-identical; GPMPC_OVERLAP=0 in
- * the environment at gpmpc_create turns it off): work queued on `stream` after the call still
- * sees the whole step complete. */
+ * side stream forked from and joined back into `stream` (results bit-identical;
+ * gpmpc_set_tuning(GPMPC_TUNE_OVERLAP, 0) turns it off): work queued on `stream` after the call
+ * still sees the whole step complete. */
 gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const int32_t* tstep, double* u0,
                          int32_t* status, int32_t* sqp_iter, int32_t* qp_iter, double* res, void* stream);
 
@@ -191,6 +192,44 @@ gpmpc_status gpmpc_plant_step(gpmpc_handle* h, int32_t batch, const double* para
  *             does nothing.
  * Results are identical up to floating-point rounding; a performance option. */
 gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves);
+
+/* What gpmpc_solve would run for `batch` instances with the current options (host, no device
+ * work): waves per instance of the SQP launch, and overlapped = 1 when a step with a variance
+ * launch runs as two overlapped halves (see gpmpc_solve).  With overlapped = 1 the profiling
+ * events of gpmpc_kernel_times bracket the costlier half's variance launch ("variance") and the
+ * span from its end to the join of both halves' SQP launches ("SQP", which also contains the
+ * cheaper half's variance launch): spans of the step, not per-kernel durations. */
+gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* waves, int32_t* overlapped);
+
+/* Performance switches (no reference counterpart; every output is bit-identical or identical up
+ * to rounding whichever value is set -- A/B measurement knobs, all on their default after
+ * gpmpc_create).  gpmpc_set_tuning(h, option, value):
+ *   GPMPC_TUNE_LIN_CACHE   1 (default): the first SQP iteration of a step reads the stored
+ *                          iterate's linearisation; 0: recompute it (bit-identical)
+ *   GPMPC_TUNE_ORDER       1 (default): a launch needing more than one round of workgroups runs
+ *                          its instances by decreasing previous cost; 0: instance order; 2: rank
+ *                          every launch (bit-identical)
+ *   GPMPC_TUNE_OVERLAP     1 (default): overlapped halves for multi-round steps; 0: sequential
+ *   GPMPC_TUNE_VAR_SPLIT   0 (default): automatic; 1: one wave per 16-point tile of the
+ *                          triangular variance kernel; 4: its four-wave column split
+ *   GPMPC_TUNE_EVENT_FENCE 0 (default): profiling events without the system-scope fence;
+ *                          1: default (fenced) events */
+enum {
+    GPMPC_TUNE_LIN_CACHE = 0,
+    GPMPC_TUNE_ORDER = 1,
+    GPMPC_TUNE_OVERLAP = 2,
+    GPMPC_TUNE_VAR_SPLIT = 3,
+    GPMPC_TUNE_EVENT_FENCE = 4
+};
+gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value);
+
+/* Optional device buffer [max_batch][H+1] (float64) receiving, on every gpmpc_solve, the stage
+ * costs of each instance's new solution: the acados LINEAR_LS cost 1/2 ||y_k - y_ref,k||^2_W with
+ * W = blkdiag(Q, R) scaled by dt on stages 0..H-1 and W_e = Q unscaled on stage H
+ * (gpmpc/gpmpc.py:231-239, gpmpc/mpc.py:101-102, acados cost_scaling), y_k = [x_k; u_k],
+ * y_ref,k = [reference window; u_eq].  Their sum is the objective value acados reports ("cost").
+ * A failed solve (status 1 or 4) writes NaN.  NULL disables (default). */
+gpmpc_status gpmpc_set_cost_buffer(gpmpc_handle* h, void* cost_dev);
 
 /* Kernel timing with HIP events recorded on the solve stream around the variance kernel
  * and the SQP kernel of every gpmpc_solve while enabled.  gpmpc_kernel_times synchronises

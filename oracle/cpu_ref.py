@@ -11,7 +11,10 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libcpuref.so"
+import os
+
+# CPUREF_LIB: another build of the same source (the sanitizer build of tools/asan_cpu_ref.sh)
+LIB_PATH = Path(os.environ.get("CPUREF_LIB", Path(__file__).resolve().parent / "lib" / "libcpuref.so"))
 _P, _I, _D = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
 _SIGS = {
     "cpuref_create": (_P, [_I, _I, _P, _I, _D, _P, _P, _P, _P, _P, _P, _P, _D, _I]),

@@ -157,3 +157,5 @@ def test_emulated_shard_line_on_the_gpu():
     assert out["cpu_baseline"] is None and out["scaling"] == "strong"
     assert abs(out["value"] - 128 * 2 / (out["ms_per_step"] * 2e-3)) <= 1e-6 * out["value"]
     assert sum(out["status_counts"].values()) == 128 * 2
+    # the shard's statistics are normalised by its own instances (no all-reduce in shard mode)
+    assert out["sqp_iter_mean"] >= 1.0 and out["linearisations_per_step"] >= 1.0

@@ -104,10 +104,10 @@ def test_launch_option_validation():
     q3.set_launch(waves=0)
 
 
-def test_cost_ordered_dispatch_is_bit_exact(monkeypatch):
+def test_cost_ordered_dispatch_is_bit_exact():
     """A launch with more instances than the device holds at once (quad3d: one instance per CU)
     dispatches them by decreasing previous-solve cost (StateDev::order); which CU runs an instance
-    when must not change any output bit: same closed loop with GPMPC_ORDER=0 (instance order)."""
+    when must not change any output bit: same closed loop with GPMPC_TUNE_ORDER 0 (instance order)."""
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
@@ -118,9 +118,9 @@ def test_cost_ordered_dispatch_is_bit_exact(monkeypatch):
     mats = lqr(spec)
     gpp = product_gps(data, hyp)
     outs = []
-    for order in ("1", "0"):
-        monkeypatch.setenv("GPMPC_ORDER", order)   # read by gpmpc_create
+    for order in (1, 0):
         gs = BatchSolver(spec, H, B)
+        gs.set_tuning(order=order)
         gs.set_gps(gpp)
         gs.set_tightening(True, 0.95, *mats)
         gs.reset(reset_iterate=True)

@@ -163,6 +163,7 @@ def test_closed_loop_parity(name, N, H, B, steps, M, love):
         assert all(r is not None for r in solver.love_ranks), solver.love_ranks
     solver.set_tightening(True, 0.95, *mats)
     solver.reset(reset_iterate=True)
+    solver.set_cost_output(True)
     sd = spec.to_dict()
     opts = O.SQPOptions(tol_stat=tol, tol_eq=tol, tol_ineq=tol, tol_comp=tol, qp_tol=1e-11)
     orc = [O.SQPSolver(sd, O.Dynamics(sd, gpo), H, opts) for _ in range(B)]
@@ -176,9 +177,14 @@ def test_closed_loop_parity(name, N, H, B, steps, M, love):
         u0 = solver.solve(xt, ts).cpu().numpy()
         st = solver.status.cpu().numpy()
         xs, us, tight = (a.cpu().numpy() for a in solver.solution())
+        cost = solver.stage_cost.cpu().numpy()
         for b in range(B):
             so, sc, ic = oracle_step(spec, orc[b], gpo, x0[b], phase[b] + step, H, traj, prev[b], lqr_mats=mats)
             assert st[b] == so == 0, (step, b, st[b], so)
+            # stage costs (acados LINEAR_LS, dt-scaled stages, unscaled terminal) of the GPU solution
+            # against the same costs of the oracle's solution
+            co = O.stage_costs(sd, orc[b].x, orc[b].u, traj, phase[b] + step)
+            np.testing.assert_allclose(cost[b], co, rtol=0, atol=1e-6 * (1.0 + co.sum()))
             scale = 1.0 + np.abs(orc[b].x).max()
             np.testing.assert_allclose(xs[b], orc[b].x, rtol=0, atol=1e-6 * scale)
             np.testing.assert_allclose(us[b], orc[b].u, rtol=0, atol=1e-6 * (1 + np.abs(orc[b].u).max()))
@@ -302,15 +308,23 @@ def test_closed_loop_parity_vs_cpp_restatement(name, N, H, B, steps, var):
     gs.set_gps(gpp)
     gs.set_tightening(True, 0.95, *mats)
     gs.reset(reset_iterate=True)
+    gs.set_cost_output(True)
     traj = spec.reference_trajectory()
+    sd = spec.to_dict()
     x0, phase = initial_states(spec, traj, B)
-    plant = O.Dynamics(spec.to_dict(), None, params=spec.true_params)
+    plant = O.Dynamics(sd, None, params=spec.true_params)
     for s in range(steps):
         gs.solve(torch.tensor(x0, device="cuda"), torch.tensor(phase + s, dtype=torch.int32, device="cuda"))
         u0 = ref.step(x0, phase + s, threads=4).copy()
         xg, ug, _ = (t.cpu().numpy() for t in gs.solution())
         st = gs.status.cpu().numpy()
         np.testing.assert_array_equal(st, ref.status)
+        # stage costs of the GPU solution (kernel) against the same costs of the C++ solution
+        cost = gs.stage_cost.cpu().numpy()
+        for b in range(B):
+            co = O.stage_costs(sd, ref.x[b], ref.u[b], traj, phase[b] + s)
+            bound = 1e-6 if st[b] == 0 else 1e-4
+            np.testing.assert_allclose(cost[b], co, rtol=0, atol=bound * (1.0 + co.sum()))
         # the same SQP iterations on both sides (the QP counts may differ by an IPM iteration where a
         # residual sits at the 1e-11 QP tolerance)
         np.testing.assert_array_equal(gs.sqp_iter.cpu().numpy(), ref.sqp_iter)

@@ -150,10 +150,10 @@ def test_mpc_q_r_weights_change_the_solution():
 
 
 @pytest.mark.parametrize("model,H,n", [("quad2d", 30, 200), ("quad3d", 15, 60)])
-def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
+def test_linearisation_cache_is_bit_exact(model, H, n):
     """The first SQP iteration of a step reads the stored iterate's linearisation (written by the
     step that produced the iterate) instead of recomputing it.  Against a solver with the cache off
-    (GPMPC_LIN_CACHE=0) every output is bit-identical over a closed loop that also re-uploads the
+    (gpmpc_set_tuning(GPMPC_TUNE_LIN_CACHE, 0)) every output is bit-identical over a closed loop that also re-uploads the
     GPs without a reset, switches the GPs off and on, changes the prior model's parameters, re-uploads
     with a reset, sets the iterate from outside and resets the multipliers (each of which must
     invalidate the cache or leave it valid)."""
@@ -173,10 +173,10 @@ def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
         return s
 
     on = make()
-    monkeypatch.setenv("GPMPC_LIN_CACHE", "0")
     off = make()
-    monkeypatch.delenv("GPMPC_LIN_CACHE")
+    off.set_tuning(lin_cache=0)
     traj = spec.reference_trajectory()
+    n_maxiter = []
     x0, ph = initial_states(spec, traj, B)
     x = torch.tensor(x0, device="cuda")
     ts = torch.tensor(ph, dtype=torch.int32, device="cuda")
@@ -215,8 +215,18 @@ def test_linearisation_cache_is_bit_exact(model, H, n, monkeypatch):
             # accepted by the reference, gpmpc.py:365) -- the latter after the perturbations above, where
             # QPs solved to the NLP tolerance (acados' default) leave a residual just above it
             st = outs[0][1]
-            assert ((st == 0) | (st == 2)).all() and (st == 0).float().mean() >= 0.8, (k, st)
+            assert ((st == 0) | (st == 2)).all(), (k, st)
+            n_maxiter.append(int((st == 2).sum()))
         x = on.plant_step(x, outs[0][0])
+    if model == "quad2d":
+        # status census of this closed loop at the default tolerances (NLP 1e-6, QP tol = NLP tol):
+        # the instance-steps stopped at the SQP iteration limit, pinned (profiles/r5/census_lincache.txt)
+        print("status-2 instance-steps per step:", n_maxiter)
+        assert sum(n_maxiter) <= LINCACHE_MAXITER_STEPS, n_maxiter
+
+
+# status-2 (SQP iteration limit) instance-steps of test_linearisation_cache_is_bit_exact's quad2d loop
+LINCACHE_MAXITER_STEPS = 3
 
 
 def test_variance_readback_only_after_a_variance_launch():
@@ -251,12 +261,12 @@ def test_variance_readback_only_after_a_variance_launch():
 
 
 @pytest.mark.parametrize("model,H,n,B", [("quad2d", 30, 200, 1100), ("cartpole", 20, 50, 1100), ("quad3d", 12, 60, 300)])
-def test_overlapped_step_is_bit_exact(model, H, n, B, monkeypatch):
+def test_overlapped_step_is_bit_exact(model, H, n, B):
     """A step whose SQP launch needs more than one round of workgroups (more instances than the
     device holds at once: 4 per CU for the one-wave models here, 1 for quad3d) runs as two
     cost-ranked halves, the second half's variance and SQP launches on a side stream beside the
     first half's SQP launch (gpmpc_solve).
-    Against a solver with the overlap off (GPMPC_OVERLAP=0: one variance launch, then one SQP
+    Against a solver with the overlap off (GPMPC_TUNE_OVERLAP 0: one variance launch, then one SQP
     launch) every output, the iterate and the tightening variances are bit-identical over a closed
     loop (the ranking changes from step to step with the instances' costs)."""
     torch = _torch()
@@ -273,9 +283,9 @@ def test_overlapped_step_is_bit_exact(model, H, n, B, monkeypatch):
         return s
 
     on = make()
-    monkeypatch.setenv("GPMPC_OVERLAP", "0")
     off = make()
-    monkeypatch.delenv("GPMPC_OVERLAP")
+    off.set_tuning(overlap=0)
+    assert on.launch_info()["overlapped"] and not off.launch_info()["overlapped"]
     x0, ph = initial_states(spec, spec.reference_trajectory(), B)
     x = torch.tensor(x0, device="cuda")
     ts = torch.tensor(ph, dtype=torch.int32, device="cuda")

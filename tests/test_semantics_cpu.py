@@ -84,3 +84,41 @@ def test_cpp_restatement_infeasible_obs_is_status_4_and_recovers():
     assert (ref.has_prev == [1, 0, 0]).all()               # next step untightened, as after a reset
     ref.step(x0, ph + 2)
     assert (ref.status == 0).all() and np.isfinite(ref.x).all()
+
+
+def test_stage_costs_are_the_linear_ls_objective_of_the_oracle():
+    """oracle.stage_costs (acados LINEAR_LS, `gpmpc/gpmpc.py:231-239`: W = blkdiag(Q, R), W_e = Q,
+    dt cost scaling on stages 0..T-1) is the objective whose gradient and Gauss-Newton Hessian the
+    oracle's SQP uses: d/dw sum_k cost_k = hdiag (w - y_ref), checked by central differences on every
+    decision variable of a random trajectory (stage-0 state included: a constant of the QP)."""
+    spec, _, _ = problem("quad2d", 10)
+    sd = spec.to_dict()
+    T, nx, nu = 6, spec.nx, spec.nu
+    rng = np.random.default_rng(4)
+    traj = spec.reference_trajectory()
+    x = traj[:, 3:3 + T + 1].T + 0.1 * rng.standard_normal((T + 1, nx))
+    u = spec.u_eq + 0.05 * rng.standard_normal((T, nu))
+    sol = O.SQPSolver(sd, O.Dynamics(sd, None), T, O.SQPOptions())
+    c = O.stage_costs(sd, x, u, traj, 3)
+    assert c.shape == (T + 1,) and (c > 0).all()
+    xr = O.reference_window(traj, 3, T).T
+    yref = sol._pack(xr, np.repeat(spec.u_eq[None, :], T, axis=0))
+    grad = sol.hdiag * (sol._pack(x, u) - yref)          # the oracle's cost gradient over [u_k; x_k+1]
+    h = 1e-6
+    for j in range(grad.size):
+        k, v = divmod(j, nx + nu)
+        xp, up, xm, um = x.copy(), u.copy(), x.copy(), u.copy()
+        if v < nu:
+            up[k, v] += h
+            um[k, v] -= h
+        else:
+            xp[k + 1, v - nu] += h
+            xm[k + 1, v - nu] -= h
+        fd = (O.stage_costs(sd, xp, up, traj, 3).sum() - O.stage_costs(sd, xm, um, traj, 3).sum()) / (2 * h)
+        assert abs(fd - grad[j]) <= 1e-7 * (1 + abs(grad[j])), (j, fd, grad[j])
+    # stage 0's state term: dt-scaled Q, like every non-terminal stage
+    x2 = x.copy()
+    x2[0] += 0.01
+    d0 = O.stage_costs(sd, x2, u, traj, 3)[0] - c[0]
+    e0 = x[0] - xr[0]
+    assert abs(d0 - 0.5 * spec.dt * (((e0 + 0.01) ** 2 - e0 ** 2) @ spec.q_diag)) <= 1e-14
