@@ -224,6 +224,9 @@ def parse_args(argv=None):
                     help="IPM tolerance of the QP sub-problems (default: the NLP tolerance 1e-6, as acados passes its "
                          "NLP tolerances on to the QP solver)")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
+    ap.add_argument("--seg", type=int, choices=[0, 1], default=None,
+                    help="two-segment Newton solves on launches with two or four waves per instance "
+                         "(gpmpc_set_tuning GPMPC_TUNE_SEG; default: the library's)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
@@ -391,6 +394,8 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         synchronize, max over ranks."""
         B = len(ids)
         solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
+        if args.seg is not None:
+            solver.set_tuning(seg=args.seg)
         solver.set_gps(gps, fitc=fitc, variance=args.variance)
         solver.set_tightening(True, 0.95, *lqr_mats)
         solver.reset(reset_iterate=True)

@@ -283,7 +283,7 @@ __device__ __attribute__((noinline)) void gp_tiles_dispatch(const double* tX, co
 template <int ID>
 constexpr int kDefaultWaves = (Model<ID>::NB + 1 > 16) ? 4 : 1;
 
-template <int ID, int NW = kDefaultWaves<ID>>
+template <int ID, int NW = kDefaultWaves<ID>, bool SEG = false>
 struct SqpKernel {
     using M = Model<ID>;
     static constexpr int NX = M::NX, NU = M::NU, NB = M::NB, NGP = M::NGP, NUNC = M::NUNC;
@@ -316,10 +316,27 @@ struct SqpKernel {
     static_assert(NW == 1 || NW == 4 || (NW == 2 && kMfma), "one wave per instance, two (single-tile models) or four: one per SIMD");
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
+    // Two-segment Newton solves (kSeg): the horizon splits at SM = H / 2; wave 0
+    // factorises stages 0..SM-1 over z = [x; 1; lambda] from the terminal cost lambda' x_SM (lambda
+    // the unknown costate of x_SM, solved for at the boundary), wave 1 stages SM..H-1 from the true
+    // P'_H, both at the same time.  lambda takes tile slots LI .. LI + NX - 1; a P' block then also
+    // carries P_x,lambda (NX x NX at PXL) and K'_k = [K | kff | K_lambda] (row stride KST).
+    static constexpr bool kSeg = SEG;
+    static_assert(!SEG || (NW >= 2 && NB + 1 <= 16 && NX + 1 <= 8), "two-segment solve: single-tile models on >= 2 waves");
+    static constexpr int LI = 8 + NU;
+    static_assert(!SEG || LI + NX <= 16, "lambda slots in the 16-wide tile");
+    static constexpr int KST = SEG ? 2 * NX + 1 : PS;          // K' row stride
+    static constexpr int PPB = SEG ? PP + NX * NX : PP;        // P' block stride
+    static constexpr int PXL = PP;                             // offset of P_x,lambda in a P' block
+    // segment boundary data (doubles): the factorised tile of stage 0 (16 x 16, row-major), lambda,
+    // x_SM, T^-1 (NX x NX), V_lambda,1 of the corrector, per-lane partial sums (64)
+    static constexpr int SB_V = 0, SB_LAM = 256, SB_XM = SB_LAM + 8, SB_TI = SB_XM + 8, SB_VL1 = SB_TI + NX * NX,
+                         SB_PART = SB_VL1 + 8, SB = SEG ? SB_PART + 64 : 0;
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
         double *G, *P, *K, *Rui, *hq, *gq, *dxv, *cd, *Acl, *dummy, *zero, *gz, *gc, *gs, *gsh;
+        double* sb;                  // kSeg: segment boundary data (SB doubles)
         double *Dq, *xs;             // WSPL: step-vector exchange, reduction slots
         double *lam, *pim;           // the instance's multipliers during the step (acados memory):
                                      // bounds [H+1][2 NB], dynamics [H][NX]
@@ -336,7 +353,7 @@ struct SqpKernel {
     }
     // P'_k of every stage boundary | GP scratch
     __host__ __device__ static size_t p_region(int H) {
-        const size_t pp = (size_t)(H + 1) * PP;
+        const size_t pp = (size_t)(H + 1) * PPB;
         return pp > gp_scratch(H) ? pp : gp_scratch(H);
     }
     __host__ __device__ static size_t lds_doubles(int H) {
@@ -344,8 +361,9 @@ struct SqpKernel {
                               + (size_t)8                    // zero slots (branch-free masked loads)
                               + (size_t)8                    // GP helper command slot
                               + (lds_mult ? (size_t)(H + 1) * 2 * NB + (size_t)H * NX : 0)   // multipliers
+                              + (size_t)SB                   // segment boundary data (kSeg)
                               + (size_t)H * NX * GS            // G'_k
-                              + (size_t)H * NU * PS          // K'_k
+                              + (size_t)H * NU * KST         // K'_k
                               + (size_t)H * NU * NU          // Ru_k^-1
                               + (size_t)(H + 1) * NBS * 2    // hq, gq (stage stride NBS)
                               + (size_t)(H + 1) * NX;        // dx (forward sweep; WSPL: the published residual)
@@ -368,8 +386,9 @@ struct SqpKernel {
             L.lam = s; s += (size_t)(H + 1) * 2 * NB;
             L.pim = s; s += (size_t)H * NX;
         }
+        L.sb = s;  s += SB;
         L.G = s;   s += (size_t)H * NX * GS;
-        L.K = s;   s += (size_t)H * NU * PS;
+        L.K = s;   s += (size_t)H * NU * KST;
         L.Rui = s; s += (size_t)H * NU * NU;
         L.hq = s;  s += (size_t)(H + 1) * NBS;
         L.gq = s;  s += (size_t)(H + 1) * NBS;
@@ -1367,6 +1386,642 @@ struct SqpKernel {
         }
     }
 
+    // ------------------------------------------------------------------ two-segment Newton solve (kSeg)
+    // Segment A = stages 0 .. SM-1 on wave 0, segment B = stages SM .. H-1 on wave 1 (tools/seg2_proto.py
+    // is the numpy model of every step below against the dense KKT solve).
+    __host__ __device__ static int seg_split(int H) { return H / 2; }
+    __device__ static int lam_of(int t) { return (t >= LI && t < LI + NX) ? t - LI : -1; }
+
+    // Riccati factorisation of stages k0 .. k1-1, mfma_backward_h's stage.  AUG (segment A): over
+    // z = [x; 1; lambda] from the terminal cost lambda' x_k1; else (segment B, k1 = H) from the true P'_H.
+    // The lambda blocks add no MFMA to the stage: the lambda rows of G'' are the identity, so
+    //   W' = P' G''          = P'[:, 0..7] G''[0..7, :] + (P' on the lambda columns)   C-init of W's first MFMA
+    //   M' = G''^T W' + D    = G''[0..7, :]^T W'[0..7, :] + (W' on the lambda rows, D elsewhere)
+    // and the Schur MFMA P'_k = M' + M'_{.u} K' covers all 16 columns (K_lambda rides in K').  Stores per
+    // stage: packed P and p (AUG: + P_x,lambda at PXL), K' = [K | kff (| K_lambda)], Ru^-1; AUG: the
+    // stage-k0 tile V (row-major 16 x 16) into the boundary data.
+    template <bool AUG>
+    __device__ static bool seg_factor(const Lds& L, int H, int lane, int k0, int k1) {
+        const int lr = lane >> 4, lc = lane & 15;
+        constexpr int CI = NX, UI = 8, NR = AUG ? 4 : 2;
+        static_assert(NX + 1 <= 8 && NU <= 2 && UI + NU <= 16, "homogeneous tile layout");
+        auto gcol = [](int t) { return t < NX ? t : (t == CI ? NB : ((t >= UI && t < UI + NU) ? NX + t - UI : -1)); };
+        auto svar = [](int t) { return t < NX ? t : ((t >= UI && t < UI + NU) ? NX + t - UI : -1); };
+        const int gc_lc = gcol(lc), sv_lc = svar(lc), lm_lc = AUG ? lam_of(lc) : -1;
+        double pn[NR];
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int t = lr + 4 * r;
+            double v = 0.0;
+            if constexpr (AUG) {   // lambda' x_k1: P'[x_i][lambda_i] = P'[lambda_i][x_i] = 1
+                v = ((t < NX && lm_lc == t) || (lam_of(t) >= 0 && lam_of(t) == lc)) ? 1.0 : 0.0;
+            } else {               // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
+                if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NBS + t] : 0.0;
+                else if (t < NX && lc == CI) v = L.gq[H * NBS + t];
+                else if (t == CI && lc < NX) v = L.gq[H * NBS + lc];
+            }
+            pn[r] = v;
+        }
+        if constexpr (!AUG) {   // P'_H (packed) for the multiplier recovery of stage H-1
+            double* PH = L.P + (size_t)H * PPB;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int t = lr + 4 * r;
+                if (t < NX) {
+                    if (lc == CI) PH[PO + t] = pn[r];
+                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
+                }
+            }
+        }
+        bool ok = true;
+        const double* pg[2];
+        int gst[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int t = lr + 4 * s2;
+            const bool ld = t < NX && gc_lc >= 0;
+            const bool one = t == CI && lc == CI;
+            pg[s2] = ld ? L.G + (size_t)(k1 - 1) * NX * GS + t * GS + gc_lc : L.zero + (one ? 7 : 0);
+            gst[s2] = ld ? NX * GS : 0;
+        }
+        const double* pd[3];
+        int dst[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int t = lr + 4 * r, sv_t = svar(t);
+            const double* base = L.zero;
+            bool on = false;
+            if (sv_t >= 0 && t == lc) { base = L.hq + sv_t; on = true; }
+            else if (sv_t >= 0 && lc == CI) { base = L.gq + sv_t; on = true; }
+            else if (t == CI && sv_lc >= 0) { base = L.gq + sv_lc; on = true; }
+            pd[r] = on ? base + (size_t)(k1 - 1) * NBS : L.zero;
+            dst[r] = on ? NBS : 0;
+        }
+        struct Stage { double g[2], d[3]; };
+        auto load_stage = [&](Stage& st) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                st.g[q] = *pg[q];
+                pg[q] -= gst[q];
+            }
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                st.d[q] = *pd[q];
+                pd[q] -= dst[q];
+            }
+        };
+        double* sp[2];
+        int sp_st[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int t = lr + 4 * r;
+            const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc) || lm_lc >= 0);
+            const int idx = (lc == CI) ? PO + t
+                                       : (lm_lc >= 0 ? PXL + t * NX + lm_lc : pidx(t < lc ? t : lc, t < lc ? lc : t));
+            sp[r] = st ? L.P + (size_t)(k1 - 1) * PPB + idx : L.dummy;
+            sp_st[r] = st ? PPB : 0;
+        }
+        const int kcol = lc < NX ? lc : (lc == CI ? NX : (lm_lc >= 0 ? NX + 1 + lm_lc : -1));
+        const bool kst = lr < NU && kcol >= 0;
+        double* sk = kst ? L.K + (size_t)(k1 - 1) * NU * KST + lr * KST + kcol : L.dummy;
+        const int sk_st = kst ? NU * KST : 0;
+        const bool rst = lane < NU * NU;
+        double* srui = rst ? L.Rui + (size_t)(k1 - 1) * NU * NU + lane : L.dummy;
+        const int srui_st = rst ? NU * NU : 0;
+        // C-init masks of the lambda blocks: columns (W') and rows of elements 2, 3 (M')
+        const bool lamc = lm_lc >= 0;
+        const bool lam2 = AUG && lam_of(lr + 8) >= 0, lam3 = AUG && lam_of(lr + 12) >= 0;
+        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
+        bool pend = false;
+        auto flush = [&]() {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                *sp[r] = pend_p[r];
+                sp[r] -= sp_st[r];
+            }
+            *sk = pend_k;
+            sk -= sk_st;
+            *srui = pend_r;
+            srui -= srui_st;
+        };
+        auto flush_at = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            if (pend) flush();
+            __builtin_amdgcn_sched_barrier(0);
+            pend = true;
+        };
+        auto stage = [&](const Stage& sd) {
+            f64x4 cw = {0.0, 0.0, 0.0, 0.0};
+            if constexpr (AUG) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) cw[r] = lamc ? pn[r] : 0.0;
+            }
+            f64x4 w = mfma64(pn[0], sd.g[0], cw);
+            w = mfma64(pn[1], sd.g[1], w);
+            flush_at();
+            f64x4 cm = {sd.d[0], sd.d[1], sd.d[2], 0.0};
+            if constexpr (AUG) {
+                cm[2] = lam2 ? w[2] : sd.d[2];
+                cm[3] = lam3 ? w[3] : 0.0;
+            }
+            f64x4 m = mfma64(sd.g[0], w[0], cm);
+            m = mfma64(sd.g[1], w[1], m);
+            double Ru[NU][NU];
+#pragma unroll
+            for (int a = 0; a < NU; ++a)
+#pragma unroll
+                for (int b2 = a; b2 < NU; ++b2) {
+                    Ru[a][b2] = readlane_d(m[2], (a << 4) | (UI + b2));
+                    Ru[b2][a] = Ru[a][b2];
+                }
+            const double mu = m[2];
+            double kb, Ri[NU][NU];
+            if constexpr (NU == 1) {
+                ok = ok && (Ru[0][0] > 0.0);
+                const double id = fast_rcp(Ru[0][0]);
+                Ri[0][0] = id;
+                kb = -id * mu;
+            } else {
+                const double det = Ru[0][0] * Ru[1][1] - Ru[0][1] * Ru[0][1];
+                ok = ok && (Ru[0][0] > 0.0) && (det > 0.0);
+                const double mo = xor16_d(mu);
+                const double num = fma((lr & 1) ? Ru[0][0] : Ru[1][1], mu, -Ru[0][1] * mo);
+                const double r0 = __builtin_amdgcn_rcp(det);
+                const double e = fma(-det, r0, 1.0);
+                const double ee = fma(e, e, e);
+                const double t = num * -r0;
+                const double id = fma(r0, ee, r0);
+                kb = fma(t, ee, t);
+                Ri[0][0] = Ru[1][1] * id;
+                Ri[1][1] = Ru[0][0] * id;
+                Ri[0][1] = Ri[1][0] = -Ru[0][1] * id;
+            }
+            const f64x4 pk = mfma64(lr < NU ? mu : 0.0, kb, m);   // P'_k = M' + M'_{.u} K'
+            double rv = Ri[0][0];
+            if constexpr (NU == 2) rv = (lane == 0) ? Ri[0][0] : ((lane == 3) ? Ri[1][1] : Ri[0][1]);
+            pend_p[0] = pk[0];
+            pend_p[1] = pk[1];
+            pend_k = kb;
+            pend_r = rv;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) pn[r] = pk[r];
+        };
+        Stage s0, s1;
+        load_stage(s0);
+        int k = k1 - 1;
+        for (; k >= k0 + 1; k -= 2) {
+            load_stage(s1);
+            stage(s0);
+            if (k >= k0 + 2) load_stage(s0);
+            stage(s1);
+        }
+        if (k == k0) stage(s0);
+        flush();
+        if constexpr (AUG) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) L.sb[SB_V + (lr + 4 * r) * 16 + lc] = pn[r];
+        }
+        return ok;
+    }
+
+    // Closed-loop stage maps A'_k = [A + B K | B kff + c] of stages k0 .. k1-1 (acl_phase over a range,
+    // K' row stride KST); only the affine column when the feedback is unchanged.
+    template <bool full>
+    __device__ static void seg_acl(const Lds& L, int lane, int k0, int k1) {
+        if constexpr (full) {
+            for (int e = k0 * NX + lane; e < k1 * NX; e += 64) {
+                const int k = e / NX, i = e - k * NX;
+                const double* G = L.G + (size_t)k * NX * GS + i * GS;
+                const double* Kk = L.K + (size_t)k * NU * KST;
+                double g[GS], kr[NU][PS];
+#pragma unroll
+                for (int j = 0; j < GS; ++j) g[j] = G[j];
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j < PS; ++j) kr[a][j] = Kk[a * KST + j];
+                double* out = L.Acl + (size_t)k * NX * PS + i * PS;
+#pragma unroll
+                for (int j = 0; j < PS; ++j) {
+                    double acc = (j < NX) ? g[j] : g[NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc = fma(g[NX + a], kr[a][j], acc);
+                    out[j] = acc;
+                }
+            }
+        } else {
+            const int n = k1 * NX;
+            for (int e0 = k0 * NX + lane; e0 < n; e0 += 192) {
+                double acc[3];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const int e = min(e0 + 64 * r, n - 1);
+                    const int k = e / NX, i = e - k * NX;
+                    const double* G = L.G + (size_t)k * NX * GS + i * GS;
+                    const double* Kk = L.K + (size_t)k * NU * KST;
+                    acc[r] = G[NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) acc[r] = fma(G[NX + a], Kk[a * KST + NX], acc[r]);
+                }
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const int e = e0 + 64 * r;
+                    if (e < n) {
+                        const int k = e / NX, i = e - k * NX;
+                        L.Acl[(size_t)k * NX * PS + i * PS + NX] = acc[r];
+                    }
+                }
+            }
+        }
+    }
+
+    // Forward sweep of stages k0 .. k1-1 from dx_k0 = xs (NULL: 0), mfma4_forward over a range; dx_k0 is
+    // stored, dx_k1 only when store_end (segment A leaves x_SM to segment B, which starts from it).
+    __device__ static void seg_forward(const Lds& L, int lane, int k0, int k1, const double* xs, bool store_end) {
+        const Mfma4Lane q = mfma4_lane(lane);
+        const bool ld = q.row < NX && q.col <= NX;
+        const double* src = ld ? L.Acl + (size_t)k0 * NX * PS + q.row * PS + q.col
+                               : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0);
+        const int st = ld ? NX * PS : 0;
+        const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+        const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+        double* dx0 = L.dxv + (size_t)k0 * NX;
+        double* out = stlo ? dx0 + NX + q.r : (sthi ? dx0 + NX + 4 + q.r : L.dummy);
+        const int ost = (stlo || sthi) ? NX : 0;
+        if (lane < NX) dx0[lane] = xs ? xs[lane] : 0.0;
+        double y = xs ? mfma4_vec(q, [&](int i) { return xs[i]; }) : mfma4_vec(q, [](int) { return 0.0; });
+        const int n = k1 - k0;
+        double an = *src;
+        for (int k = 0; k < n; ++k) {
+            const double a = an;
+            src += (k + 1 < n) ? st : 0;
+            an = *src;
+            double sv;
+            y = mfma4_stage(a, y, sv);
+            if (store_end || k + 1 < n) *out = sv;
+            out += ost;
+        }
+    }
+
+    // Corrector right-hand side over stages k0 .. k1-1 (mfma4_vector_backward over a range): last
+    // (segment B): from the true p_H; else (segment A) from the zero terminal P_k1 = 0, p_k1 = 0, plus
+    // V_lambda,1 = sum_k P_lambda,x,k+1 (c_k + B_k kff_k) (P_lambda,x,k1 = I) into the boundary data.
+    __device__ static void seg_vector_backward(const Lds& L, int H, int lane, int k0, int k1, bool last) {
+        double* T = L.hq;
+        double* VT = L.dxv;
+        const int n = k1 * NX;
+        auto t_entry = [&](int e) {
+            const int k = e / NX, i = e - k * NX;
+            const double* Pn = L.P + (size_t)(k + 1) * PPB;
+            const double* G = L.G + (size_t)k * NX * GS;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
+            return (last || k + 1 < k1) ? acc : 0.0;
+        };
+        for (int e0 = k0 * NX + lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            T[e0] = a0;
+            if (has1) T[e1] = a1;
+        }
+        WSYNC();
+        auto vt_entry = [&](int e) {
+            const int k = e / NX, i = e - k * NX;
+            const double* A = L.Acl + (size_t)k * NX * PS;
+            const double* Kk = L.K + (size_t)k * NU * KST;
+            double acc = L.gq[k * NBS + i];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * KST + i], L.gq[k * NBS + NX + a], acc);
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
+            return acc;
+        };
+        for (int e0 = k0 * NX + lane; e0 < n; e0 += 128) {
+            const int e1 = e0 + 64;
+            const bool has1 = e1 < n;
+            const double a0 = vt_entry(e0), a1 = vt_entry(has1 ? e1 : e0);
+            VT[e0] = a0;
+            if (has1) VT[e1] = a1;
+        }
+        WSYNC();
+        {
+            const Mfma4Lane q = mfma4_lane(lane);
+            const bool lda = q.row < NX && q.col < NX, ldv = q.row < NX && q.col == NX;
+            const double* src = lda ? L.Acl + (size_t)(k1 - 1) * NX * PS + q.col * PS + q.row
+                                    : (ldv ? VT + (size_t)(k1 - 1) * NX + q.row
+                                           : L.zero + ((q.row == NX && q.col == NX) ? 7 : 0));
+            const int st = lda ? NX * PS : (ldv ? NX : 0);
+            if (last && lane < NX) L.P[(size_t)H * PPB + PO + lane] = L.gq[H * NBS + lane];
+            double y = last ? mfma4_vec(q, [&](int i) { return L.gq[H * NBS + i]; }) : mfma4_vec(q, [](int) { return 0.0; });
+            const bool stlo = q.b == 0 && q.c == 0 && q.r < NX;
+            const bool sthi = q.b == 2 && q.c == 0 && 4 + q.r < NX;
+            double* out = stlo ? L.P + (size_t)(k1 - 1) * PPB + PO + q.r
+                               : (sthi ? L.P + (size_t)(k1 - 1) * PPB + PO + 4 + q.r : L.dummy);
+            const int ost = (stlo || sthi) ? PPB : 0;
+            double an = *src;
+            for (int k = k1 - 1; k >= k0; --k) {
+                const double a = an;
+                src -= (k >= k0 + 1) ? st : 0;
+                an = *src;
+                double sv;
+                y = mfma4_stage(a, y, sv);
+                *out = sv;
+                out -= ost;
+            }
+        }
+        WSYNC();
+        for (int e = k0 * NU + lane; e < k1 * NU; e += 64) {
+            const int k = e / NU, a = e - k * NU;
+            const double* G = L.G + (size_t)k * NX * GS;
+            const bool pz = !last && k + 1 == k1;   // segment end: p_k1 = 0
+            const double* pn = L.P + (size_t)(k + 1) * PPB + PO;
+            double kf = 0.0;
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                double acc = L.gq[k * NBS + NX + b2];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + NX + b2], T[k * NX + l] + (pz ? 0.0 : pn[l]), acc);
+                kf = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], acc, kf);
+            }
+            L.K[(size_t)k * NU * KST + a * KST + NX] = -kf;
+        }
+        WSYNC();
+        if (!last) {
+            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k, z_k = c_k + B_k kff_k: lane (k, j) forms term j of
+            // stage k into VT (its p-recurrence input is consumed), then lanes j < NX add the terms
+            for (int e = k0 * NX + lane; e < n; e += 64) {
+                const int k = e / NX, j = e - k * NX;
+                const double* G = L.G + (size_t)k * NX * GS;
+                const double* Kk = L.K + (size_t)k * NU * KST + NX;
+                const double* Pl = L.P + (size_t)(k + 1) * PPB + PXL;
+                double acc = 0.0;
+#pragma unroll
+                for (int t = 0; t < NX; ++t) {
+                    double z = G[t * GS + NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) z = fma(G[t * GS + NX + a], Kk[a * KST], z);
+                    acc = (k + 1 == k1) ? (t == j ? z : acc) : fma(Pl[t * NX + j], z, acc);
+                }
+                VT[e] = acc;
+            }
+            WSYNC();
+            if (lane < NX) {
+                double acc = 0.0;
+                for (int k = k0; k < k1; ++k) acc += VT[k * NX + lane];
+                L.sb[SB_VL1 + lane] = acc;
+            }
+            WSYNC();
+        }
+    }
+
+    // Predictor boundary (wave 1, after both factorisations).  Ph, ph: the true cost-to-go at SM (segment
+    // B's P'_SM), V: segment A's stage-0 tile.  lambda = Ph x_SM + ph and x_SM = V_l1 + V_ll lambda give
+    //   T lambda = Ph V_l1 + ph,   T = I - Ph V_ll,
+    // solved by Gauss-Jordan with partial pivoting, lane c holding column c of [T | r | I] (rows in
+    // registers; the pivot column is read by v_readlane, so the pivot choice is uniform).  T^-1 stays in
+    // the boundary data for the corrector.  Then x_SM.
+    __device__ static void seg_boundary_full(const Lds& L, int H, int lane) {
+        constexpr int CI = NX;
+        const double* Pm = L.P + (size_t)seg_split(H) * PPB;
+        const double* V = L.sb + SB_V;
+        double pk[PP];
+#pragma unroll
+        for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
+        const int c = min(lane, 2 * NX);
+        double b[NX];
+#pragma unroll
+        for (int l = 0; l < NX; ++l)
+            b[l] = c < NX ? -V[(LI + l) * 16 + LI + c] : (c == NX ? V[(LI + l) * 16 + CI] : 0.0);
+        double col[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = c < NX ? (i == c ? 1.0 : 0.0) : (c == NX ? pk[PO + i] : (i == c - NX - 1 ? 1.0 : 0.0));
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], b[l], acc);
+            col[i] = acc;
+        }
+#pragma unroll
+        for (int p = 0; p < NX; ++p) {
+            double cp[NX];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
+            int piv = p;
+            double best = fabs(cp[p]);
+#pragma unroll
+            for (int i = p + 1; i < NX; ++i)
+                if (fabs(cp[i]) > best) { best = fabs(cp[i]); piv = i; }
+#pragma unroll
+            for (int i = p + 1; i < NX; ++i) {
+                if (piv == i) {
+                    const double t0 = col[p]; col[p] = col[i]; col[i] = t0;
+                    const double t1 = cp[p]; cp[p] = cp[i]; cp[i] = t1;
+                }
+            }
+            const double inv = 1.0 / cp[p];
+            col[p] *= inv;
+#pragma unroll
+            for (int i = 0; i < NX; ++i)
+                if (i != p) col[i] = fma(-cp[i], col[p], col[i]);
+        }
+        if (lane == NX) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) L.sb[SB_LAM + i] = col[i];
+        } else if (lane > NX && lane <= 2 * NX) {
+#pragma unroll
+            for (int i = 0; i < NX; ++i) L.sb[SB_TI + i * NX + (lane - NX - 1)] = col[i];
+        }
+        double lam[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lam[j] = readlane_d(col[j], NX);
+        if (lane < NX) {
+            double acc = V[(LI + lane) * 16 + CI];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(V[(LI + lane) * 16 + LI + j], lam[j], acc);
+            L.sb[SB_XM + lane] = acc;
+        }
+        WSYNC();
+    }
+
+    // Corrector boundary (wave 1): the factorisation is unchanged, so T^-1 and Ph are; new ph (segment
+    // B's p_SM from its vector sweep) and V_l1 (segment A's): lambda = T^-1 (Ph V_l1 + ph), x_SM.
+    __device__ static void seg_boundary_vec(const Lds& L, int H, int lane) {
+        constexpr int CI = NX;
+        (void)CI;
+        const double* Pm = L.P + (size_t)seg_split(H) * PPB;
+        const double* V = L.sb + SB_V;
+        const int i = min(lane, NX - 1);
+        double vl[NX];
+#pragma unroll
+        for (int l = 0; l < NX; ++l) vl[l] = L.sb[SB_VL1 + l];
+        double r = Pm[PO + i];
+#pragma unroll
+        for (int l = 0; l < NX; ++l) r = fma(Pm[i <= l ? pidx(i, l) : pidx(l, i)], vl[l], r);
+        double rv[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) rv[j] = readlane_d(r, j);
+        double lv = 0.0;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lv = fma(L.sb[SB_TI + i * NX + j], rv[j], lv);
+        double lam[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lam[j] = readlane_d(lv, j);
+        if (lane < NX) {
+            L.sb[SB_LAM + lane] = lv;
+            double acc = vl[lane < NX ? lane : 0];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(V[(LI + lane) * 16 + LI + j], lam[j], acc);
+            L.sb[SB_XM + lane] = acc;
+        }
+        WSYNC();
+    }
+
+    // Segment A's feedforward with the solved boundary costate: kff_k += K_lambda,k lambda (k < SM).
+    __device__ static void seg_fold(const Lds& L, int H, int lane) {
+        double lam[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lam[j] = L.sb[SB_LAM + j];
+        for (int e = lane; e < seg_split(H) * NU; e += 64) {
+            double* kr = L.K + (size_t)e * KST;
+            double acc = kr[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(kr[NX + 1 + j], lam[j], acc);
+            kr[NX] = acc;
+        }
+    }
+
+    // Per-lane step from the two-segment solution: recover_step_mfma with the KST / PPB strides, and
+    // inside segment A the costate of x_{k+1} adds P_x,lambda,k+1 lambda (the boundary's costate).
+    __device__ static void recover_step_seg(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        const bool on = lane <= H;
+        const int kk = min(lane, H - 1);
+        double dx[NX], dxn[NX];
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            dx[i] = (on && lane >= 1) ? L.dxv[(size_t)lane * NX + i] : 0.0;
+            dxn[i] = L.dxv[(size_t)(kk + 1) * NX + i];
+        }
+#pragma unroll
+        for (int i = 0; i < NX; ++i) dd[i] = dx[i];
+#pragma unroll
+        for (int a = 0; a < NU; ++a) {
+            double kr[PS];
+#pragma unroll
+            for (int j = 0; j < PS; ++j) kr[j] = L.K[(size_t)kk * NU * KST + a * KST + j];
+            double du = kr[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) du = fma(kr[j], dx[j], du);
+            dd[NX + a] = (lane < H) ? du : 0.0;
+        }
+        const double* Pn = L.P + (size_t)(kk + 1) * PPB;
+        const bool inA = kk + 1 < seg_split(H);
+        double lam[NX];
+#pragma unroll
+        for (int j = 0; j < NX; ++j) lam[j] = inA ? L.sb[SB_LAM + j] : 0.0;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            double acc = Pn[PO + i];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(Pn[i <= j ? pidx(i, j) : pidx(j, i)], dxn[j], acc);
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(inA ? Pn[PXL + i * NX + j] : 0.0, lam[j], acc);
+            dpi[i] = (lane < H) ? -acc : 0.0;
+        }
+    }
+
+    // The two-segment solves, posted by wave 0 to the helper waves (helper_loop, seg_helper).  Wave 1
+    // runs segment A (the lambda recursion) and the boundary; segment B runs on wave 2 when the instance
+    // has four waves, so that wave 0 -- whose registers hold the IPM state -- only posts and waits, and on
+    // wave 0 itself with two waves (segment B is mfma_backward_h's recursion over a range: no more
+    // registers than the one-segment kernel's).
+    //   kCmdSegFactor (predictor): B1 | factorisations A / B + closed-loop maps | Bm1 | wave 1: boundary |
+    //                 Bm2 | forward sweeps A (after kff += K_lambda lambda) / B | B2
+    //   kCmdSegVector (corrector): B1 | vector passes A / B | Bm1 | wave 1: boundary | Bm2 | forward | B2
+    // Other waves only meet the barriers.  Factorisation statuses: ctrl[8] (A), ctrl[9] (B).
+    static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
+    static constexpr int kSegBWave = NW >= 4 ? 2 : 0;
+    __device__ static void seg_b_factor(const Lds& L, int H, int lane) {
+        const int SM = seg_split(H);
+        const bool ok = seg_factor<false>(L, H, lane, SM, H);
+        WSYNC();
+        seg_acl<true>(L, lane, SM, H);
+        if (lane == 0) L.ctrl[9] = ok ? 1 : 0;
+    }
+    __device__ static bool seg_predictor(const Lds& L, int H, int lane) {
+        if (lane == 0) L.ctrl[0] = kCmdSegFactor;
+        __syncthreads();   // B1
+        if constexpr (kSegBWave == 0) seg_b_factor(L, H, lane);
+        __syncthreads();   // Bm1
+        const bool ok = L.ctrl[8] != 0 && L.ctrl[9] != 0;
+        __syncthreads();   // Bm2: lambda, x_SM
+        if constexpr (kSegBWave == 0) {
+            if (ok) seg_forward(L, lane, seg_split(H), H, L.sb + SB_XM, true);
+        }
+        __syncthreads();   // B2
+        return ok;
+    }
+    __device__ static void seg_corrector(const Lds& L, int H, int lane) {
+        const int SM = seg_split(H);
+        if (lane == 0) L.ctrl[0] = kCmdSegVector;
+        __syncthreads();   // B1
+        if constexpr (kSegBWave == 0) seg_vector_backward(L, H, lane, SM, H, true);
+        __syncthreads();   // Bm1
+        __syncthreads();   // Bm2: lambda, x_SM
+        if constexpr (kSegBWave == 0) {
+            seg_acl<false>(L, lane, SM, H);
+            WSYNC();
+            seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
+        }
+        __syncthreads();   // B2
+    }
+    // helper wave w's part of a two-segment command (after B1)
+    __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
+        const int SM = seg_split(H);
+        const bool segA = w == 1, segB = kSegBWave != 0 && w == kSegBWave;
+        if (cmd == kCmdSegFactor) {
+            if (segA) {
+                const bool ok = seg_factor<true>(L, H, lane, 0, SM);
+                WSYNC();
+                seg_acl<true>(L, lane, 0, SM);
+                if (lane == 0) L.ctrl[8] = ok ? 1 : 0;
+            }
+            if (segB) seg_b_factor(L, H, lane);
+            __syncthreads();   // Bm1
+            const bool ok = L.ctrl[8] != 0 && L.ctrl[9] != 0;
+            if (segA && ok) seg_boundary_full(L, H, lane);
+            __syncthreads();   // Bm2
+            if (segA && ok) {
+                seg_fold(L, H, lane);
+                WSYNC();
+                seg_acl<false>(L, lane, 0, SM);
+                WSYNC();
+                seg_forward(L, lane, 0, SM, nullptr, false);
+            }
+            if (segB && ok) seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
+            __syncthreads();   // B2
+        } else {
+            if (segA) seg_vector_backward(L, H, lane, 0, SM, false);
+            if (segB) seg_vector_backward(L, H, lane, SM, H, true);
+            __syncthreads();   // Bm1
+            if (segA) seg_boundary_vec(L, H, lane);
+            __syncthreads();   // Bm2
+            if (segA) {
+                seg_fold(L, H, lane);
+                WSYNC();
+                seg_acl<false>(L, lane, 0, SM);
+                WSYNC();
+                seg_forward(L, lane, 0, SM, nullptr, false);
+            }
+            if (segB) {
+                seg_acl<false>(L, lane, SM, H);
+                WSYNC();
+                seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
+            }
+            __syncthreads();   // B2
+        }
+    }
+
     // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
     __device__ static void ctpi(const Lds& L, int H, int lane, const double (&pi)[NX], double (&out)[NB]) {
         double pim1[NX];
@@ -1452,7 +2107,8 @@ struct SqpKernel {
     template <int NV>
     __device__ static void recover_q(const Lds& L, int H, int kq, int vb, double (&dd)[NV], double (&dp)[NX]) {
         double ddf[NB];
-        if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
+        if constexpr (kSeg) recover_step_seg(L, H, kq, ddf, dp);
+        else if constexpr (kMfma) recover_step_mfma(L, H, kq, ddf, dp);
         else recover_step(L, H, kq, ddf, dp);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
@@ -1692,7 +2348,14 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(4);
                 double dd[NV], dp[NX];
-                if constexpr (kMfma) {
+                if constexpr (kSeg) {
+                    // two-segment solve on waves 0 and 1 (seg_predictor)
+                    const bool rok = seg_predictor(L, H, lane);
+                    if (!rok) { qp_ok = false; break; }
+                    TPHASE(9);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else if constexpr (kMfma) {
                     bool rok = true;
                     if (wv == 0) {   // (WSPL: the other waves wait at the status exchange)
                         rok = mfma_backward_h(L, H, lane);
@@ -1767,7 +2430,12 @@ struct SqpKernel {
                 }
                 XSYNC();
                 TPHASE(5);
-                if constexpr (kMfma) {
+                if constexpr (kSeg) {
+                    seg_corrector(L, H, lane);
+                    TPHASE(9);
+                    recover_q<NV>(L, H, kq, vb, dd, dp);
+                    TPHASE(3);
+                } else if constexpr (kMfma) {
                     if (wv == 0) {
                         mfma4_vector_backward(L, H, lane);
                         TPHASE(8);
@@ -1852,6 +2520,12 @@ struct SqpKernel {
             __syncthreads();   // B1
             const int G = L.ctrl[0];
             if (G == -1) break;
+            if constexpr (kSeg) {   // a two-segment Newton solve (seg_predictor / seg_corrector)
+                if (G == kCmdSegFactor || G == kCmdSegVector) {
+                    seg_helper(L, H, lane, w, G);
+                    continue;
+                }
+            }
             if constexpr (WSPL) {
                 if (G == -2) {
                     constexpr int NV = nv_of<false>();
@@ -2416,18 +3090,18 @@ __global__ __launch_bounds__(256) void order_by_cost_kernel(const uint32_t* __re
 }
 
 // One wave per SIMD: every wave of an instance owns a SIMD's register file.
-template <int ID, int NW, bool SPL>
+template <int ID, int NW, bool SPL, bool SEG = false>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_step_kernel(ProblemDev P, StateDev S, StepIO io) {
-    SqpKernel<ID, NW>::template run<SPL>(P, S, io);
+    SqpKernel<ID, NW, SEG>::template run<SPL>(P, S, io);
 }
 // count < 0: the whole batch (ordered by cost here when it needs more than one round of workgroups);
 // count >= 0: ranks first .. first + count - 1 of an order[] launch_sqp_order already filled
-template <int ID, int NW, bool SPL>
+template <int ID, int NW, bool SPL, bool SEG = false>
 hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
                               int first, int count) {
-    const size_t lds = SqpKernel<ID, NW>::lds_doubles(P.H) * sizeof(double);
+    const size_t lds = SqpKernel<ID, NW, SEG>::lds_doubles(P.H) * sizeof(double);
     if (lds > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL>,
+        const hipError_t e = hipFuncSetAttribute((const void*)sqp_step_kernel<ID, NW, SPL, SEG>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
@@ -2438,7 +3112,7 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
     if (count >= 0) {   // a chunk of ranks of the order already computed
         if (count == 0) return hipSuccess;
         Sl.first = first;
-        hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL>), dim3(count), dim3(64 * NW), lds, stream, P, Sl, io);
+        hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, SEG>), dim3(count), dim3(64 * NW), lds, stream, P, Sl, io);
         return hipGetLastError();
     }
     // (rank by counting: O(B^2) comparisons, a few microseconds up to ~16 k instances; larger
@@ -2452,7 +3126,7 @@ hipError_t launch_sqp_variant(const ProblemDev& P, const StateDev& S, const Step
     } else {
         Sl.order = nullptr;
     }
-    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL>), dim3(batch), dim3(64 * NW), lds, stream, P, Sl, io);
+    hipLaunchKernelGGL((sqp_step_kernel<ID, NW, SPL, SEG>), dim3(batch), dim3(64 * NW), lds, stream, P, Sl, io);
     return hipGetLastError();
 }
 
@@ -2471,6 +3145,10 @@ int sqp_waves(const ProblemDev& P, int batch) {
     }
 }
 
+// two-segment Newton solves (SqpKernel::kSeg): the single-tile models on two or four waves per
+// instance, when the option allows it (P.seg) and each segment has at least two stages
+static bool sqp_seg_of(const ProblemDev& P, int nw) { return P.seg != 0 && nw >= 2 && P.H >= 4; }
+
 template <int ID>
 hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO& io, int batch, hipStream_t stream,
                            int first, int count) {
@@ -2478,12 +3156,21 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
         // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
         const bool spl = P.H + 1 <= 32;
         const int nw = sqp_waves<ID>(P, batch);   // from the whole batch, also for a chunk of it
-        if (nw == 4)
+        const bool seg = sqp_seg_of(P, nw);
+        if (nw == 4) {
+            if (seg)
+                return spl ? launch_sqp_variant<ID, 4, true, true>(P, S, io, batch, stream, first, count)
+                           : launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
             return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream, first, count)
                        : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream, first, count);
-        if (nw == 2)
+        }
+        if (nw == 2) {
+            if (seg)
+                return spl ? launch_sqp_variant<ID, 2, true, true>(P, S, io, batch, stream, first, count)
+                           : launch_sqp_variant<ID, 2, false, true>(P, S, io, batch, stream, first, count);
             return spl ? launch_sqp_variant<ID, 2, true>(P, S, io, batch, stream, first, count)
                        : launch_sqp_variant<ID, 2, false>(P, S, io, batch, stream, first, count);
+        }
         return spl ? launch_sqp_variant<ID, 1, true>(P, S, io, batch, stream, first, count)
                    : launch_sqp_variant<ID, 1, false>(P, S, io, batch, stream, first, count);
     } else {
@@ -2504,8 +3191,9 @@ static bool overlap_ok_of(const ProblemDev& P, int batch) {
     const int nw = sqp_waves<ID>(P, batch);
     size_t lds = SqpKernel<ID>::lds_doubles(P.H);
     if constexpr (kDefaultWaves<ID> == 1) {
-        if (nw == 4) lds = SqpKernel<ID, 4>::lds_doubles(P.H);
-        if (nw == 2) lds = SqpKernel<ID, 2>::lds_doubles(P.H);
+        const bool seg = sqp_seg_of(P, nw);
+        if (nw == 4) lds = seg ? SqpKernel<ID, 4, true>::lds_doubles(P.H) : SqpKernel<ID, 4>::lds_doubles(P.H);
+        if (nw == 2) lds = seg ? SqpKernel<ID, 2, true>::lds_doubles(P.H) : SqpKernel<ID, 2>::lds_doubles(P.H);
     }
     const int per_cu = std::max(1, std::min(4 / nw, (int)((160 * 1024) / (lds * sizeof(double)))));
     return batch > P.n_cu * per_cu;

@@ -23,7 +23,7 @@ def _torch():
     return torch
 
 
-def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True):
+def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
     """all_converge: every instance-step reaches KKT 1e-9 (tools/status_census.py, profiles/r4/
     status_census.jsonl); otherwise the ones stopped at the SQP iteration limit (status 2 on both
     sides, at most one instance or 5 %) ran the same iterations from the same start and agree to 1e-4."""
@@ -40,6 +40,7 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True):
     ref = cpu_ref.CpuRef(spec, H, B, gps=gpo, lqr_mats=mats, tol=tol, qp_tol=1e-11, qp_max_iter=100)
     gs = BatchSolver(spec, H, B, tol=tol, qp_tol=1e-11, qp_max_iter=100)
     gs.set_launch(waves=waves)
+    gs.set_tuning(seg=seg)
     gs.set_gps(gpp)
     gs.set_tightening(True, 0.95, *mats)
     gs.reset(reset_iterate=True)
@@ -68,13 +69,14 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True):
     return gs
 
 
-@pytest.mark.parametrize("waves", [1, 2, 4])
+@pytest.mark.parametrize("waves,seg", [(1, 0), (2, 0), (4, 0), (2, 1), (4, 1)])
 @pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 12, 4), ("cartpole", 50, 20, 12, 4),
                                                ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
-def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves):
+def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, seg):
+    """seg = 1: the two-segment Newton solve (gpmpc_set_tuning GPMPC_TUNE_SEG) on two or four waves."""
     # quad2d N=200 H=30: one of the 12 instances needs more than 25 SQP iterations for KKT 1e-9 at
     # step 1 (Gauss-Newton's linear rate; the C++ restatement stops there too)
-    _run_against_cpp(name, N, H, B, steps, waves, all_converge=not (name == "quad2d" and H == 30))
+    _run_against_cpp(name, N, H, B, steps, waves, all_converge=not (name == "quad2d" and H == 30), seg=seg)
 
 
 def test_auto_two_waves_between_one_and_two_instances_per_cu():
