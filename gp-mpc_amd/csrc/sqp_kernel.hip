@@ -1877,22 +1877,34 @@ struct SqpKernel {
         WSYNC();
     }
 
-    // Segment A's feedforward with the solved boundary costate: kff_k += K_lambda,k lambda (k < SM).
+    // Segment A with the solved boundary costate lambda: the feedforward kff_k += K_lambda,k lambda
+    // (k < SM) and the costate vectors p_k += P_x,lambda,k lambda (0 < k < SM), so the sweep and the
+    // multiplier recovery read an ordinary one-segment factorisation (the next factorisation or
+    // corrector pass rewrites both).
     __device__ static void seg_fold(const Lds& L, int H, int lane) {
+        const int SM = seg_split(H);
         double lam[NX];
 #pragma unroll
         for (int j = 0; j < NX; ++j) lam[j] = L.sb[SB_LAM + j];
-        for (int e = lane; e < seg_split(H) * NU; e += 64) {
+        for (int e = lane; e < SM * NU; e += 64) {
             double* kr = L.K + (size_t)e * KST;
             double acc = kr[NX];
 #pragma unroll
             for (int j = 0; j < NX; ++j) acc = fma(kr[NX + 1 + j], lam[j], acc);
             kr[NX] = acc;
         }
+        for (int e = NX + lane; e < SM * NX; e += 64) {
+            const int k = e / NX, i = e - k * NX;
+            double* Pk = L.P + (size_t)k * PPB;
+            double acc = Pk[PO + i];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) acc = fma(Pk[PXL + i * NX + j], lam[j], acc);
+            Pk[PO + i] = acc;
+        }
     }
 
-    // Per-lane step from the two-segment solution: recover_step_mfma with the KST / PPB strides, and
-    // inside segment A the costate of x_{k+1} adds P_x,lambda,k+1 lambda (the boundary's costate).
+    // Per-lane step from the two-segment solution: recover_step_mfma with the KST / PPB strides (the
+    // boundary costate is already folded into segment A's kff and p, seg_fold).
     __device__ static void recover_step_seg(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
         const bool on = lane <= H;
         const int kk = min(lane, H - 1);
@@ -1915,17 +1927,14 @@ struct SqpKernel {
             dd[NX + a] = (lane < H) ? du : 0.0;
         }
         const double* Pn = L.P + (size_t)(kk + 1) * PPB;
-        const bool inA = kk + 1 < seg_split(H);
-        double lam[NX];
+        double pp[PP];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) lam[j] = inA ? L.sb[SB_LAM + j] : 0.0;
+        for (int q = 0; q < PP; ++q) pp[q] = Pn[q];
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
-            double acc = Pn[PO + i];
+            double acc = pp[PO + i];
 #pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(Pn[i <= j ? pidx(i, j) : pidx(j, i)], dxn[j], acc);
-#pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(inA ? Pn[PXL + i * NX + j] : 0.0, lam[j], acc);
+            for (int j = 0; j < NX; ++j) acc = fma(pp[i <= j ? pidx(i, j) : pidx(j, i)], dxn[j], acc);
             dpi[i] = (lane < H) ? -acc : 0.0;
         }
     }

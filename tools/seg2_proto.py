@@ -138,7 +138,8 @@ def seg2_solve(A, B, c, h, g, H, nx, nu, m):
         out[k, :nx], out[k, nx:] = x, u
         x = A[k] @ x + B[k] @ u + c[k]
     out[H, :nx] = x
-    for k in range(H):   # dpi_k = -(P_{k+1} dx_{k+1} + p_{k+1} (+ P_x,lambda lambda inside segment A))
+    for k in range(H):   # dpi_k = -(P_{k+1} dx_{k+1} + p_{k+1} (+ P_x,lambda lambda inside segment A: the
+                         # kernel folds it into p_{k+1}, seg_fold)
         Pn = P[k + 1]
         v = Pn[:nx, :nx] @ out[k + 1, :nx] + Pn[:nx, CI]
         if k + 1 < m:
