@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference")
     ap.add_argument("--dump", default="", help="save the per-step per-instance phase cycles (.npy)")
     ap.add_argument("--waves", type=int, default=0, help="waves per instance (gpmpc_set_launch; 0 = auto)")
+    ap.add_argument("--seg", type=int, default=None, help="two-segment Newton solves (gpmpc_set_tuning GPMPC_TUNE_SEG)")
     args = ap.parse_args()
     from gpmpc import _lib
     from gpmpc.gp import GaussianProcess
@@ -58,6 +59,8 @@ def main():
     mats = setup_prior_dynamics(dfdx, dfdu, np.diag(spec.q_diag), np.diag(spec.r_diag), spec.dt)
     s = BatchSolver(spec, H, B)
     s.set_launch(waves=args.waves)
+    if args.seg is not None:
+        s.set_tuning(seg=args.seg)
     if args.no_gp:
         s.set_gps(None)
     else:
