@@ -467,6 +467,10 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
     status_counts, maxes = m["status_counts"], m["maxes"]
 
     if rank == 0 or emulated:   # an emulated shard is the only process: it always reports
+        # a step run as overlapped halves (gpmpc_get_launch_info): the events bracket spans of the step
+        # (the costlier half's variance launch; then both SQP launches plus the cheaper half's
+        # variance launch), not kernel durations -- no per-kernel figure is derived from them
+        overlapped = m["launch"]["overlapped"]
         per_lin, exps_lin, var_flops = gp_flops(spec, N, H, getattr(solver, "love_ranks", None))
         # dominant kernel: the SQP kernel; linearisations computed per instance-step = sqp_iter + 1,
         # minus the one read from the linearisation cache (lin_mean, counted by the kernel)
@@ -493,10 +497,6 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
                                    f"of this command, committed; 2 x FETCH + WRITE per launch)")
         except (OSError, ValueError, KeyError):
             traffic = None
-        # a step run as overlapped halves (gpmpc_get_launch_info): the events bracket spans of the step
-        # (the costlier half's variance launch; then both SQP launches plus the cheaper half's
-        # variance launch), not kernel durations -- no per-kernel figure is derived from them
-        overlapped = m["launch"]["overlapped"]
         single = None
         if world == 1 and not emulated and not args.no_single_instance and not args.fitc:
             single = single_instance_gpu(spec, gps, H, lqr_mats, m["x0_all"][ids.start], m["phase_all"][ids.start],
