@@ -214,10 +214,10 @@ gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* wave
  *                          triangular variance kernel; 4: its four-wave column split
  *   GPMPC_TUNE_EVENT_FENCE 0 (default): profiling events without the system-scope fence;
  *                          1: default (fenced) events
- *   GPMPC_TUNE_SEG         two-segment Newton solves when a launch runs two or four waves per
- *                          instance (quad2d, cartpole): the horizon's two halves are factorised
- *                          and swept on two waves at once and joined at the boundary (1), or one
- *                          wave runs the whole recursion (0); identical up to rounding */
+ *   GPMPC_TUNE_SEG         1 (default): two-segment Newton solves when a launch runs two or four
+ *                          waves per instance (quad2d, cartpole): the horizon's two halves are
+ *                          factorised and swept on two waves at once and joined at the boundary;
+ *                          0: one wave runs the whole recursion; identical up to rounding */
 enum {
     GPMPC_TUNE_LIN_CACHE = 0,
     GPMPC_TUNE_ORDER = 1,
