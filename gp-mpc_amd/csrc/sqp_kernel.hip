@@ -1749,19 +1749,19 @@ struct SqpKernel {
         }
         WSYNC();
         if (!last) {
-            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k, z_k = c_k + B_k kff_k: lane (k, j) forms term j of
+            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k with z_k = c_k + B_k kff_k, the affine column of the
+            // closed-loop map A'_k (seg_acl<false> with this pass's kff): lane (k, j) forms term j of
             // stage k into VT (its p-recurrence input is consumed), then lanes j < NX add the terms
+            seg_acl<false>(L, lane, k0, k1);
+            WSYNC();
             for (int e = k0 * NX + lane; e < n; e += 64) {
                 const int k = e / NX, j = e - k * NX;
-                const double* G = L.G + (size_t)k * NX * GS;
-                const double* Kk = L.K + (size_t)k * NU * KST + NX;
+                const double* Ak = L.Acl + (size_t)k * NX * PS + NX;
                 const double* Pl = L.P + (size_t)(k + 1) * PPB + PXL;
                 double acc = 0.0;
 #pragma unroll
                 for (int t = 0; t < NX; ++t) {
-                    double z = G[t * GS + NB];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) z = fma(G[t * GS + NX + a], Kk[a * KST], z);
+                    const double z = Ak[t * PS];
                     acc = (k + 1 == k1) ? (t == j ? z : acc) : fma(Pl[t * NX + j], z, acc);
                 }
                 VT[e] = acc;
@@ -1819,7 +1819,7 @@ struct SqpKernel {
                     const double t1 = cp[p]; cp[p] = cp[i]; cp[i] = t1;
                 }
             }
-            const double inv = 1.0 / cp[p];
+            const double inv = fast_rcp(cp[p]);
             col[p] *= inv;
 #pragma unroll
             for (int i = 0; i < NX; ++i)
@@ -1881,25 +1881,35 @@ struct SqpKernel {
     // (k < SM) and the costate vectors p_k += P_x,lambda,k lambda (0 < k < SM), so the sweep and the
     // multiplier recovery read an ordinary one-segment factorisation (the next factorisation or
     // corrector pass rewrites both).
+    // The closed-loop affine column A'_k[:, CI] = c_k + B_k kff_k follows in the same pass
+    // (+ B_k K_lambda,k lambda), so no closed-loop pass runs between the fold and the forward sweep.
     __device__ static void seg_fold(const Lds& L, int H, int lane) {
         const int SM = seg_split(H);
         double lam[NX];
 #pragma unroll
         for (int j = 0; j < NX; ++j) lam[j] = L.sb[SB_LAM + j];
-        for (int e = lane; e < SM * NU; e += 64) {
-            double* kr = L.K + (size_t)e * KST;
-            double acc = kr[NX];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(kr[NX + 1 + j], lam[j], acc);
-            kr[NX] = acc;
-        }
-        for (int e = NX + lane; e < SM * NX; e += 64) {
+        for (int e = lane; e < SM * NX; e += 64) {
             const int k = e / NX, i = e - k * NX;
-            double* Pk = L.P + (size_t)k * PPB;
-            double acc = Pk[PO + i];
+            const double* Kk = L.K + (size_t)k * NU * KST;
+            double dk[NU];   // K_lambda,k lambda
 #pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(Pk[PXL + i * NX + j], lam[j], acc);
-            Pk[PO + i] = acc;
+            for (int a = 0; a < NU; ++a) {
+                double acc = 0.0;
+#pragma unroll
+                for (int j = 0; j < NX; ++j) acc = fma(Kk[a * KST + NX + 1 + j], lam[j], acc);
+                dk[a] = acc;
+            }
+            const double* G = L.G + (size_t)k * NX * GS + i * GS;
+            double ac = L.Acl[(size_t)k * NX * PS + i * PS + NX];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) ac = fma(G[NX + a], dk[a], ac);
+            double* Pk = L.P + (size_t)k * PPB;
+            double pv = Pk[PO + i];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) pv = fma(Pk[PXL + i * NX + j], lam[j], pv);
+            L.Acl[(size_t)k * NX * PS + i * PS + NX] = ac;
+            if (k >= 1) Pk[PO + i] = pv;
+            if (i < NU) L.K[(size_t)k * NU * KST + i * KST + NX] += dk[i < NU ? i : 0];
         }
     }
 
@@ -2003,8 +2013,6 @@ struct SqpKernel {
             if (segA && ok) {
                 seg_fold(L, H, lane);
                 WSYNC();
-                seg_acl<false>(L, lane, 0, SM);
-                WSYNC();
                 seg_forward(L, lane, 0, SM, nullptr, false);
             }
             if (segB && ok) seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
@@ -2017,8 +2025,6 @@ struct SqpKernel {
             __syncthreads();   // Bm2
             if (segA) {
                 seg_fold(L, H, lane);
-                WSYNC();
-                seg_acl<false>(L, lane, 0, SM);
                 WSYNC();
                 seg_forward(L, lane, 0, SM, nullptr, false);
             }

@@ -44,7 +44,7 @@ __device__ void init_data(const typename KS<ID>::Lds& L, int H, int lane, int sa
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-// V: 0 factor A, 1 factor B, 2 boundary (predictor), 3 fold + acl + forward A, 4 forward B,
+// V: 0 factor A, 1 factor B, 2 boundary (predictor), 3 fold + forward A, 4 forward B,
 //    5 vector backward A (+ V_l1), 6 vector backward B, 7 boundary (corrector), 8 acl<true> A
 template <int ID, int V>
 __global__ __launch_bounds__(256) void micro(int H, int reps, unsigned long long* out, double* sink) {
@@ -63,8 +63,6 @@ __global__ __launch_bounds__(256) void micro(int H, int reps, unsigned long long
         if constexpr (V == 2) K::seg_boundary_full(L, H, lane);
         if constexpr (V == 3) {
             K::seg_fold(L, H, lane);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            K::template seg_acl<false>(L, lane, 0, SM);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             K::seg_forward(L, lane, 0, SM, nullptr, false);
         }
@@ -106,7 +104,7 @@ int main() {
         run<kQuad2D, 1>("quad2d factor B (15 stages)", H, B, reps, d_out, d_sink);
         run<kQuad2D, 8>("quad2d acl<true> A", H, B, reps, d_out, d_sink);
         run<kQuad2D, 2>("quad2d boundary (predictor, GJ)", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 3>("quad2d fold + acl<false> + forward A", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 3>("quad2d fold + forward A", H, B, reps, d_out, d_sink);
         run<kQuad2D, 4>("quad2d forward B", H, B, reps, d_out, d_sink);
         run<kQuad2D, 5>("quad2d vector backward A (+ V_l1)", H, B, reps, d_out, d_sink);
         run<kQuad2D, 6>("quad2d vector backward B", H, B, reps, d_out, d_sink);
