@@ -316,11 +316,12 @@ struct SqpKernel {
     static_assert(NW == 1 || NW == 4 || (NW == 2 && kMfma), "one wave per instance, two (single-tile models) or four: one per SIMD");
     static constexpr int PP = NX * (NX + 1) / 2 + NX;   // packed P (upper triangle) + p
     static constexpr int PO = NX * (NX + 1) / 2;        // offset of p in a packed P' block
-    // Two-segment Newton solves (kSeg): the horizon splits at SM = H / 2; wave 0
-    // factorises stages 0..SM-1 over z = [x; 1; lambda] from the terminal cost lambda' x_SM (lambda
-    // the unknown costate of x_SM, solved for at the boundary), wave 1 stages SM..H-1 from the true
-    // P'_H, both at the same time.  lambda takes tile slots LI .. LI + NX - 1; a P' block then also
-    // carries P_x,lambda (NX x NX at PXL) and K'_k = [K | kff | K_lambda] (row stride KST).
+    // Segment-parallel Newton solves (kSeg): the horizon splits into NSEG segments
+    // (three on four waves, two on two), factorised and swept at the same time on different waves;
+    // every segment but the last runs over z = [x; 1; lambda] from the terminal cost lambda' x_b (lambda
+    // the unknown costate of its end state x_b, solved for by the boundary chain), the last from the
+    // true P'_H.  lambda takes tile slots LI .. LI + NX - 1; a P' block then also carries P_x,lambda
+    // (NX x NX at PXL) and K'_k = [K | kff | K_lambda] (row stride KST).
     static constexpr bool kSeg = SEG;
     static_assert(!SEG || (NW >= 2 && NB + 1 <= 16 && NX + 1 <= 8), "two-segment solve: single-tile models on >= 2 waves");
     static constexpr int LI = 8 + NU;
@@ -328,10 +329,15 @@ struct SqpKernel {
     static constexpr int KST = SEG ? 2 * NX + 1 : PS;          // K' row stride
     static constexpr int PPB = SEG ? PP + NX * NX : PP;        // P' block stride
     static constexpr int PXL = PP;                             // offset of P_x,lambda in a P' block
-    // segment boundary data (doubles): the factorised tile of stage 0 (16 x 16, row-major), lambda,
-    // x_SM, T^-1 (NX x NX), V_lambda,1 of the corrector, per-lane partial sums (64)
-    static constexpr int SB_V = 0, SB_LAM = 256, SB_XM = SB_LAM + 8, SB_TI = SB_XM + 8, SB_VL1 = SB_TI + NX * NX,
-                         SB_PART = SB_VL1 + 8, SB = SEG ? SB_PART + 64 : 0;
+    static constexpr int NSEG = NW >= 4 ? 3 : 2;   // segments: waves 1, 2, 3 (four waves) or 1, 0 (two)
+    static constexpr int NBD = NSEG - 1;            // boundaries
+    // segment boundary data (doubles): per boundary b (segment b's end) the factorised tile of the
+    // segment's first stage (16 x 16, row-major), lambda_b, the segment's V_lambda,1 of the corrector,
+    // T_b^-1, Y_b, y_b and the true cost-to-go at s_{b+1} when the chain computed it (packed P, p);
+    // per segment its start state x_w
+    static constexpr int SB_V = 0, SB_LAM = SB_V + 256 * NBD, SB_XM = SB_LAM + 8 * NBD, SB_VL1 = SB_XM + 8 * NSEG,
+                         SB_TI = SB_VL1 + 8 * NBD, SB_Y = SB_TI + NX * NX * NBD, SB_YV = SB_Y + NX * NX * NBD,
+                         SB_PH = SB_YV + 8 * NBD, SB = SEG ? SB_PH + PP * NBD : 0;
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
@@ -1386,10 +1392,10 @@ struct SqpKernel {
         }
     }
 
-    // ------------------------------------------------------------------ two-segment Newton solve (kSeg)
-    // Segment A = stages 0 .. SM-1 on wave 0, segment B = stages SM .. H-1 on wave 1 (tools/seg2_proto.py
-    // is the numpy model of every step below against the dense KKT solve).
-    __host__ __device__ static int seg_split(int H) { return H / 2; }
+    // ------------------------------------------------------------------ segment-parallel Newton solve (kSeg)
+    // Segment w = stages seg_start(w) .. seg_start(w + 1) - 1 on wave seg_wave(w) (tools/seg2_proto.py
+    // is the numpy model of the two-segment form against the dense KKT solve).
+    __host__ __device__ static int seg_start(int w, int H) { return (w * H) / NSEG; }
     __device__ static int lam_of(int t) { return (t >= LI && t < LI + NX) ? t - LI : -1; }
 
     // Riccati factorisation of stages k0 .. k1-1, mfma_backward_h's stage.  AUG (segment A): over
@@ -1401,7 +1407,7 @@ struct SqpKernel {
     // stage: packed P and p (AUG: + P_x,lambda at PXL), K' = [K | kff (| K_lambda)], Ru^-1; AUG: the
     // stage-k0 tile V (row-major 16 x 16) into the boundary data.
     template <bool AUG>
-    __device__ static bool seg_factor(const Lds& L, int H, int lane, int k0, int k1) {
+    __device__ static bool seg_factor(const Lds& L, int H, int lane, int k0, int k1, double* vtile) {
         const int lr = lane >> 4, lc = lane & 15;
         constexpr int CI = NX, UI = 8, NR = AUG ? 4 : 2;
         static_assert(NX + 1 <= 8 && NU <= 2 && UI + NU <= 16, "homogeneous tile layout");
@@ -1579,7 +1585,7 @@ struct SqpKernel {
         flush();
         if constexpr (AUG) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) L.sb[SB_V + (lr + 4 * r) * 16 + lc] = pn[r];
+            for (int r = 0; r < 4; ++r) vtile[(lr + 4 * r) * 16 + lc] = pn[r];
         }
         return ok;
     }
@@ -1666,7 +1672,7 @@ struct SqpKernel {
     // Corrector right-hand side over stages k0 .. k1-1 (mfma4_vector_backward over a range): last
     // (segment B): from the true p_H; else (segment A) from the zero terminal P_k1 = 0, p_k1 = 0, plus
     // V_lambda,1 = sum_k P_lambda,x,k+1 (c_k + B_k kff_k) (P_lambda,x,k1 = I) into the boundary data.
-    __device__ static void seg_vector_backward(const Lds& L, int H, int lane, int k0, int k1, bool last) {
+    __device__ static void seg_vector_backward(const Lds& L, int H, int lane, int k0, int k1, bool last, double* vl1) {
         double* T = L.hq;
         double* VT = L.dxv;
         const int n = k1 * NX;
@@ -1770,125 +1776,178 @@ struct SqpKernel {
             if (lane < NX) {
                 double acc = 0.0;
                 for (int k = k0; k < k1; ++k) acc += VT[k * NX + lane];
-                L.sb[SB_VL1 + lane] = acc;
+                vl1[lane] = acc;
             }
             WSYNC();
         }
     }
 
-    // Predictor boundary (wave 1, after both factorisations).  Ph, ph: the true cost-to-go at SM (segment
-    // B's P'_SM), V: segment A's stage-0 tile.  lambda = Ph x_SM + ph and x_SM = V_l1 + V_ll lambda give
-    //   T lambda = Ph V_l1 + ph,   T = I - Ph V_ll,
-    // solved by Gauss-Jordan with partial pivoting, lane c holding column c of [T | r | I] (rows in
-    // registers; the pivot column is read by v_readlane, so the pivot choice is uniform).  T^-1 stays in
-    // the boundary data for the corrector.  Then x_SM.
-    __device__ static void seg_boundary_full(const Lds& L, int H, int lane) {
+    // Boundary chain of the predictor (wave 1, after every segment's factorisation).  Backward over the
+    // boundaries b = NSEG-2 .. 0; boundary b joins segment b (tile V: its first stage's P'_aug) to the
+    // true cost-to-go Ph, ph at s_{b+1} (the last segment's P' there, or the previous boundary's result):
+    //   T_b = I - Ph V_ll,   [Y_b | y_b] = T_b^-1 [Ph V_lx | Ph V_l1 + ph],
+    //   Ph <- V_xx + V_xl Y_b,  ph <- V_x1 + V_xl y_b          (the cost-to-go at s_b, for boundary b - 1)
+    // (lambda_b = Ph x_{b+1} + ph and x_{b+1} = V_lx x_b + V_l1 + V_ll lambda_b), by Gauss-Jordan with
+    // partial pivoting, lane c holding column c of [T | Ph V_lx | r | I] (rows in registers; the pivot
+    // column is read by v_readlane, so the pivot choice is uniform).  Then seg_chain_forward.  T_b^-1,
+    // Y_b and the computed cost-to-go matrices stay in the boundary data for the corrector.
+    __device__ static void seg_chain_full(const Lds& L, int H, int lane) {
         constexpr int CI = NX;
-        const double* Pm = L.P + (size_t)seg_split(H) * PPB;
-        const double* V = L.sb + SB_V;
-        double pk[PP];
+        const int c = min(lane, 3 * NX);
+        for (int b = NSEG - 2; b >= 0; --b) {
+            const double* V = L.sb + SB_V + b * 256;
+            const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
+            double pk[PP];
 #pragma unroll
-        for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
-        const int c = min(lane, 2 * NX);
-        double b[NX];
+            for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
+            double bv[NX];
 #pragma unroll
-        for (int l = 0; l < NX; ++l)
-            b[l] = c < NX ? -V[(LI + l) * 16 + LI + c] : (c == NX ? V[(LI + l) * 16 + CI] : 0.0);
-        double col[NX];
+            for (int l = 0; l < NX; ++l)
+                bv[l] = c < NX ? -V[(LI + l) * 16 + LI + c]
+                               : (c < 2 * NX ? V[(LI + l) * 16 + (c - NX)] : (c == 2 * NX ? V[(LI + l) * 16 + CI] : 0.0));
+            double col[NX];
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            double acc = c < NX ? (i == c ? 1.0 : 0.0) : (c == NX ? pk[PO + i] : (i == c - NX - 1 ? 1.0 : 0.0));
+            for (int i = 0; i < NX; ++i) {
+                double acc = c < NX ? (i == c ? 1.0 : 0.0)
+                                    : (c == 2 * NX ? pk[PO + i] : (c > 2 * NX ? (i == c - 2 * NX - 1 ? 1.0 : 0.0) : 0.0));
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], b[l], acc);
-            col[i] = acc;
-        }
-#pragma unroll
-        for (int p = 0; p < NX; ++p) {
-            double cp[NX];
-#pragma unroll
-            for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
-            int piv = p;
-            double best = fabs(cp[p]);
-#pragma unroll
-            for (int i = p + 1; i < NX; ++i)
-                if (fabs(cp[i]) > best) { best = fabs(cp[i]); piv = i; }
-#pragma unroll
-            for (int i = p + 1; i < NX; ++i) {
-                if (piv == i) {
-                    const double t0 = col[p]; col[p] = col[i]; col[i] = t0;
-                    const double t1 = cp[p]; cp[p] = cp[i]; cp[i] = t1;
-                }
+                for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], bv[l], acc);
+                col[i] = acc;
             }
-            const double inv = fast_rcp(cp[p]);
-            col[p] *= inv;
 #pragma unroll
-            for (int i = 0; i < NX; ++i)
-                if (i != p) col[i] = fma(-cp[i], col[p], col[i]);
+            for (int p = 0; p < NX; ++p) {
+                double cp[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
+                int piv = p;
+                double best = fabs(cp[p]);
+#pragma unroll
+                for (int i = p + 1; i < NX; ++i)
+                    if (fabs(cp[i]) > best) { best = fabs(cp[i]); piv = i; }
+#pragma unroll
+                for (int i = p + 1; i < NX; ++i) {
+                    if (piv == i) {
+                        const double t0 = col[p]; col[p] = col[i]; col[i] = t0;
+                        const double t1 = cp[p]; cp[p] = cp[i]; cp[i] = t1;
+                    }
+                }
+                const double inv = fast_rcp(cp[p]);
+                col[p] *= inv;
+#pragma unroll
+                for (int i = 0; i < NX; ++i)
+                    if (i != p) col[i] = fma(-cp[i], col[p], col[i]);
+            }
+            if (lane >= NX && lane < 2 * NX) {
+                if (b >= 1) {
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) L.sb[SB_Y + b * NX * NX + i * NX + (lane - NX)] = col[i];
+                }
+            } else if (lane == 2 * NX) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) L.sb[SB_YV + 8 * b + i] = col[i];
+            } else if (lane > 2 * NX && lane <= 3 * NX) {
+#pragma unroll
+                for (int i = 0; i < NX; ++i) L.sb[SB_TI + b * NX * NX + i * NX + (lane - 2 * NX - 1)] = col[i];
+            }
+            if (b >= 1) {
+                // cost-to-go at s_b, packed: lane NX + j (j < NX) column j of V_xx + V_xl Y_b, lane 2 NX the
+                // vector V_x1 + V_xl y_b
+                if (lane >= NX && lane <= 2 * NX) {
+                    const int j = lane - NX;
+                    double* dst = L.sb + SB_PH + (b - 1) * PP;
+#pragma unroll
+                    for (int i = 0; i < NX; ++i) {
+                        double acc = V[i * 16 + (j < NX ? j : CI)];
+#pragma unroll
+                        for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], col[l], acc);
+                        if (j == NX) dst[PO + i] = acc;
+                        else if (i <= j) dst[pidx(i, j)] = acc;
+                    }
+                }
+                WSYNC();
+            }
         }
-        if (lane == NX) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) L.sb[SB_LAM + i] = col[i];
-        } else if (lane > NX && lane <= 2 * NX) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) L.sb[SB_TI + i * NX + (lane - NX - 1)] = col[i];
-        }
-        double lam[NX];
-#pragma unroll
-        for (int j = 0; j < NX; ++j) lam[j] = readlane_d(col[j], NX);
-        if (lane < NX) {
-            double acc = V[(LI + lane) * 16 + CI];
-#pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(V[(LI + lane) * 16 + LI + j], lam[j], acc);
-            L.sb[SB_XM + lane] = acc;
-        }
-        WSYNC();
+        seg_chain_forward(L, lane);
     }
 
-    // Corrector boundary (wave 1): the factorisation is unchanged, so T^-1 and Ph are; new ph (segment
-    // B's p_SM from its vector sweep) and V_l1 (segment A's): lambda = T^-1 (Ph V_l1 + ph), x_SM.
-    __device__ static void seg_boundary_vec(const Lds& L, int H, int lane) {
+    // Forward over the boundaries from x_0 = 0: lambda_b = Y_b x_b + y_b (boundary 0: y_0),
+    // x_{b+1} = V_lx x_b + V_l1 + V_ll lambda_b; lambda_b and the segment start states x_w into the
+    // boundary data.
+    __device__ static void seg_chain_forward(const Lds& L, int lane) {
         constexpr int CI = NX;
-        (void)CI;
-        const double* Pm = L.P + (size_t)seg_split(H) * PPB;
-        const double* V = L.sb + SB_V;
         const int i = min(lane, NX - 1);
-        double vl[NX];
+        double xh[NX];
 #pragma unroll
-        for (int l = 0; l < NX; ++l) vl[l] = L.sb[SB_VL1 + l];
-        double r = Pm[PO + i];
+        for (int l = 0; l < NX; ++l) xh[l] = 0.0;
+        for (int b = 0; b < NSEG - 1; ++b) {
+            const double* V = L.sb + SB_V + b * 256;
+            double lv = L.sb[SB_YV + 8 * b + i];
+            if (b >= 1) {
 #pragma unroll
-        for (int l = 0; l < NX; ++l) r = fma(Pm[i <= l ? pidx(i, l) : pidx(l, i)], vl[l], r);
-        double rv[NX];
+                for (int l = 0; l < NX; ++l) lv = fma(L.sb[SB_Y + b * NX * NX + i * NX + l], xh[l], lv);
+            }
+            double lam[NX];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) rv[j] = readlane_d(r, j);
-        double lv = 0.0;
+            for (int j = 0; j < NX; ++j) lam[j] = readlane_d(lv, j);
+            double xn = V[(LI + i) * 16 + CI];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) lv = fma(L.sb[SB_TI + i * NX + j], rv[j], lv);
-        double lam[NX];
+            for (int l = 0; l < NX; ++l) xn = fma(V[(LI + i) * 16 + l], xh[l], xn);
 #pragma unroll
-        for (int j = 0; j < NX; ++j) lam[j] = readlane_d(lv, j);
-        if (lane < NX) {
-            L.sb[SB_LAM + lane] = lv;
-            double acc = vl[lane < NX ? lane : 0];
+            for (int j = 0; j < NX; ++j) xn = fma(V[(LI + i) * 16 + LI + j], lam[j], xn);
+            if (lane < NX) {
+                L.sb[SB_LAM + 8 * b + lane] = lv;
+                L.sb[SB_XM + 8 * (b + 1) + lane] = xn;
+            }
 #pragma unroll
-            for (int j = 0; j < NX; ++j) acc = fma(V[(LI + lane) * 16 + LI + j], lam[j], acc);
-            L.sb[SB_XM + lane] = acc;
+            for (int l = 0; l < NX; ++l) xh[l] = readlane_d(xn, l);
         }
         WSYNC();
     }
 
-    // Segment A with the solved boundary costate lambda: the feedforward kff_k += K_lambda,k lambda
-    // (k < SM) and the costate vectors p_k += P_x,lambda,k lambda (0 < k < SM), so the sweep and the
-    // multiplier recovery read an ordinary one-segment factorisation (the next factorisation or
-    // corrector pass rewrites both).
-    // The closed-loop affine column A'_k[:, CI] = c_k + B_k kff_k follows in the same pass
-    // (+ B_k K_lambda,k lambda), so no closed-loop pass runs between the fold and the forward sweep.
-    __device__ static void seg_fold(const Lds& L, int H, int lane) {
-        const int SM = seg_split(H);
+    // Boundary chain of the corrector (wave 1): the factorisation, hence T_b^-1, Y_b and the cost-to-go
+    // matrices, is unchanged; new vectors only: ph at s_{NSEG-1} from the last segment's vector pass,
+    // V_l1 and V_x1 (the segment's zero-terminal p at its start) from the others':
+    //   y_b = T_b^-1 (Ph V_l1 + ph),  ph <- V_x1 + V_xl y_b,  then seg_chain_forward.
+    __device__ static void seg_chain_vec(const Lds& L, int H, int lane) {
+        const int i = min(lane, NX - 1);
+        double phv = L.P[(size_t)seg_start(NSEG - 1, H) * PPB + PO + i];
+        for (int b = NSEG - 2; b >= 0; --b) {
+            const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
+            double r = phv;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) r = fma(Pm[i <= l ? pidx(i, l) : pidx(l, i)], L.sb[SB_VL1 + 8 * b + l], r);
+            double rv[NX];
+#pragma unroll
+            for (int j = 0; j < NX; ++j) rv[j] = readlane_d(r, j);
+            double yv = 0.0;
+#pragma unroll
+            for (int j = 0; j < NX; ++j) yv = fma(L.sb[SB_TI + b * NX * NX + i * NX + j], rv[j], yv);
+            if (lane < NX) L.sb[SB_YV + 8 * b + lane] = yv;
+            if (b >= 1) {
+                const double* V = L.sb + SB_V + b * 256;
+                double yu[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) yu[j] = readlane_d(yv, j);
+                double p1 = L.P[(size_t)seg_start(b, H) * PPB + PO + i];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) p1 = fma(V[i * 16 + LI + l], yu[l], p1);
+                phv = p1;
+            }
+        }
+        WSYNC();
+        seg_chain_forward(L, lane);
+    }
+
+    // A segment with its solved terminal costate lambda: the feedforward kff_k += K_lambda,k lambda and
+    // the costate vectors p_k += P_x,lambda,k lambda (k0 <= k < k1, k >= 1), so the sweep and the
+    // multiplier recovery read an ordinary factorisation (the next factorisation or corrector pass
+    // rewrites both); the closed-loop affine column A'_k[:, CI] = c_k + B_k kff_k follows in the same
+    // pass (+ B_k K_lambda,k lambda), so no closed-loop pass runs between the fold and the sweep.
+    __device__ static void seg_fold(const Lds& L, int lane, int k0, int k1, const double* lamp) {
         double lam[NX];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) lam[j] = L.sb[SB_LAM + j];
-        for (int e = lane; e < SM * NX; e += 64) {
+        for (int j = 0; j < NX; ++j) lam[j] = lamp[j];
+        for (int e = k0 * NX + lane; e < k1 * NX; e += 64) {
             const int k = e / NX, i = e - k * NX;
             const double* Kk = L.K + (size_t)k * NU * KST;
             double dk[NU];   // K_lambda,k lambda
@@ -1949,92 +2008,82 @@ struct SqpKernel {
         }
     }
 
-    // The two-segment solves, posted by wave 0 to the helper waves (helper_loop, seg_helper).  Wave 1
-    // runs segment A (the lambda recursion) and the boundary; segment B runs on wave 2 when the instance
-    // has four waves, so that wave 0 -- whose registers hold the IPM state -- only posts and waits, and on
-    // wave 0 itself with two waves (segment B is mfma_backward_h's recursion over a range: no more
-    // registers than the one-segment kernel's).
-    //   kCmdSegFactor (predictor): B1 | factorisations A / B + closed-loop maps | Bm1 | wave 1: boundary |
-    //                 Bm2 | forward sweeps A (after kff += K_lambda lambda) / B | B2
-    //   kCmdSegVector (corrector): B1 | vector passes A / B | Bm1 | wave 1: boundary | Bm2 | forward | B2
-    // Other waves only meet the barriers.  Factorisation statuses: ctrl[8] (A), ctrl[9] (B).
+    // The segment-parallel solves, posted by wave 0 to the helper waves (helper_loop).  Segment w runs
+    // on wave seg_wave(w): waves 1, 2, 3 with four waves, so wave 0 -- whose registers hold the IPM state
+    // -- only posts and waits; waves 1 and 0 with two (wave 0 then runs the last segment, an ordinary
+    // recursion over a range: no more registers than the one-segment kernel's).  Wave 1 also runs the
+    // boundary chain.
+    //   kCmdSegFactor (predictor): B1 | factorisations + closed-loop maps | Bm1 | wave 1: chain | Bm2 |
+    //                 forward sweeps (after the fold of each segment's lambda) | B2
+    //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain | Bm2 | forward | B2
+    // Factorisation statuses in ctrl[8 + w].
     static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
-    static constexpr int kSegBWave = NW >= 4 ? 2 : 0;
-    __device__ static void seg_b_factor(const Lds& L, int H, int lane) {
-        const int SM = seg_split(H);
-        const bool ok = seg_factor<false>(L, H, lane, SM, H);
-        WSYNC();
-        seg_acl<true>(L, lane, SM, H);
-        if (lane == 0) L.ctrl[9] = ok ? 1 : 0;
-    }
-    __device__ static bool seg_predictor(const Lds& L, int H, int lane) {
-        if (lane == 0) L.ctrl[0] = kCmdSegFactor;
-        __syncthreads();   // B1
-        if constexpr (kSegBWave == 0) seg_b_factor(L, H, lane);
-        __syncthreads();   // Bm1
-        const bool ok = L.ctrl[8] != 0 && L.ctrl[9] != 0;
-        __syncthreads();   // Bm2: lambda, x_SM
-        if constexpr (kSegBWave == 0) {
-            if (ok) seg_forward(L, lane, seg_split(H), H, L.sb + SB_XM, true);
-        }
-        __syncthreads();   // B2
-        return ok;
-    }
-    __device__ static void seg_corrector(const Lds& L, int H, int lane) {
-        const int SM = seg_split(H);
-        if (lane == 0) L.ctrl[0] = kCmdSegVector;
-        __syncthreads();   // B1
-        if constexpr (kSegBWave == 0) seg_vector_backward(L, H, lane, SM, H, true);
-        __syncthreads();   // Bm1
-        __syncthreads();   // Bm2: lambda, x_SM
-        if constexpr (kSegBWave == 0) {
-            seg_acl<false>(L, lane, SM, H);
-            WSYNC();
-            seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
-        }
-        __syncthreads();   // B2
-    }
-    // helper wave w's part of a two-segment command (after B1)
-    __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
-        const int SM = seg_split(H);
-        const bool segA = w == 1, segB = kSegBWave != 0 && w == kSegBWave;
+    __host__ __device__ static constexpr int seg_of_wave(int w) { return NSEG == 3 ? w - 1 : (w == 1 ? 0 : (w == 0 ? 1 : -1)); }
+    // KIND 0: no segment on this wave; 1: segment sg < NSEG - 1 (lambda recursion); 2: the last segment
+    template <int KIND>
+    __device__ static bool seg_part(const Lds& L, int H, int lane, int sg, bool chain, int cmd) {
+        const int k0 = seg_start(sg, H), k1 = seg_start(sg + 1, H);
+        double* xs = L.sb + SB_XM + 8 * sg;
+        bool ok = true;
         if (cmd == kCmdSegFactor) {
-            if (segA) {
-                const bool ok = seg_factor<true>(L, H, lane, 0, SM);
+            if constexpr (KIND == 1) {
+                const bool fok = seg_factor<true>(L, H, lane, k0, k1, L.sb + SB_V + sg * 256);
                 WSYNC();
-                seg_acl<true>(L, lane, 0, SM);
-                if (lane == 0) L.ctrl[8] = ok ? 1 : 0;
+                seg_acl<true>(L, lane, k0, k1);
+                if (lane == 0) L.ctrl[8 + sg] = fok ? 1 : 0;
+            } else if constexpr (KIND == 2) {
+                const bool fok = seg_factor<false>(L, H, lane, k0, H, nullptr);
+                WSYNC();
+                seg_acl<true>(L, lane, k0, H);
+                if (lane == 0) L.ctrl[8 + sg] = fok ? 1 : 0;
             }
-            if (segB) seg_b_factor(L, H, lane);
             __syncthreads();   // Bm1
-            const bool ok = L.ctrl[8] != 0 && L.ctrl[9] != 0;
-            if (segA && ok) seg_boundary_full(L, H, lane);
-            __syncthreads();   // Bm2
-            if (segA && ok) {
-                seg_fold(L, H, lane);
-                WSYNC();
-                seg_forward(L, lane, 0, SM, nullptr, false);
+#pragma unroll
+            for (int q = 0; q < NSEG; ++q) ok = ok && L.ctrl[8 + q] != 0;
+            if (chain && ok) seg_chain_full(L, H, lane);
+            __syncthreads();   // Bm2: lambda_b, x_w
+            if (ok) {
+                if constexpr (KIND == 1) {
+                    seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
+                    WSYNC();
+                    seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
+                } else if constexpr (KIND == 2) {
+                    seg_forward(L, lane, k0, H, xs, true);
+                }
             }
-            if (segB && ok) seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
             __syncthreads();   // B2
         } else {
-            if (segA) seg_vector_backward(L, H, lane, 0, SM, false);
-            if (segB) seg_vector_backward(L, H, lane, SM, H, true);
+            if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
+            if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
             __syncthreads();   // Bm1
-            if (segA) seg_boundary_vec(L, H, lane);
-            __syncthreads();   // Bm2
-            if (segA) {
-                seg_fold(L, H, lane);
+            if (chain) seg_chain_vec(L, H, lane);
+            __syncthreads();   // Bm2: lambda_b, x_w
+            if constexpr (KIND == 1) {
+                seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
                 WSYNC();
-                seg_forward(L, lane, 0, SM, nullptr, false);
-            }
-            if (segB) {
-                seg_acl<false>(L, lane, SM, H);
+                seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
+            } else if constexpr (KIND == 2) {
+                seg_acl<false>(L, lane, k0, H);
                 WSYNC();
-                seg_forward(L, lane, SM, H, L.sb + SB_XM, true);
+                seg_forward(L, lane, k0, H, xs, true);
             }
             __syncthreads();   // B2
         }
+        return ok;
+    }
+    // wave 0 (inside qp_ipm): post the command, then its own part
+    __device__ static bool seg_run(const Lds& L, int H, int lane, int cmd) {
+        if (lane == 0) L.ctrl[0] = cmd;
+        __syncthreads();   // B1
+        constexpr int sg0 = seg_of_wave(0);
+        return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, sg0 < 0 ? 0 : sg0, false, cmd);
+    }
+    // helper wave w's part of a segment command (after B1)
+    __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
+        const int sg = seg_of_wave(w);
+        if (sg == NSEG - 1) (void)seg_part<2>(L, H, lane, sg, w == 1, cmd);
+        else if (sg >= 0) (void)seg_part<1>(L, H, lane, sg, w == 1, cmd);
+        else (void)seg_part<0>(L, H, lane, 0, false, cmd);
     }
 
     // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
@@ -2364,8 +2413,8 @@ struct SqpKernel {
                 TPHASE(4);
                 double dd[NV], dp[NX];
                 if constexpr (kSeg) {
-                    // two-segment solve on waves 0 and 1 (seg_predictor)
-                    const bool rok = seg_predictor(L, H, lane);
+                    // segment-parallel solve on the helper waves (seg_run)
+                    const bool rok = seg_run(L, H, lane, kCmdSegFactor);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
@@ -2446,7 +2495,7 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(5);
                 if constexpr (kSeg) {
-                    seg_corrector(L, H, lane);
+                    (void)seg_run(L, H, lane, kCmdSegVector);
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
@@ -2535,7 +2584,7 @@ struct SqpKernel {
             __syncthreads();   // B1
             const int G = L.ctrl[0];
             if (G == -1) break;
-            if constexpr (kSeg) {   // a two-segment Newton solve (seg_predictor / seg_corrector)
+            if constexpr (kSeg) {   // a segment-parallel Newton solve (seg_run)
                 if (G == kCmdSegFactor || G == kCmdSegVector) {
                     seg_helper(L, H, lane, w, G);
                     continue;

@@ -1,4 +1,4 @@
-// Micro-benchmark of the two-segment Newton solve's pieces (SqpKernel<ID, 4, true>, diagnostic only):
+// Micro-benchmark of the segment-parallel Newton solve's pieces (SqpKernel<ID, 4, true>: three segments, diagnostic only):
 // each production device function timed alone on wave 0 of a 4-wave workgroup, on synthetic stage
 // data in LDS (tools/ric_micro.hip's), 256 instances (one per CU).  Cycles per call (s_memtime).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=1 \
@@ -32,15 +32,15 @@ __device__ void init_data(const typename KS<ID>::Lds& L, int H, int lane, int sa
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    const int SM = K::seg_split(H);
-    K::template seg_factor<false>(L, H, lane, SM, H);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    K::template seg_acl<true>(L, lane, SM, H);
-    K::template seg_factor<true>(L, H, lane, 0, SM);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    K::template seg_acl<true>(L, lane, 0, SM);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    K::seg_boundary_full(L, H, lane);
+    for (int w = K::NSEG - 1; w >= 0; --w) {
+        const int k0 = K::seg_start(w, H), k1 = K::seg_start(w + 1, H);
+        if (w == K::NSEG - 1) K::template seg_factor<false>(L, H, lane, k0, k1, nullptr);
+        else K::template seg_factor<true>(L, H, lane, k0, k1, L.sb + K::SB_V + 256 * w);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        K::template seg_acl<true>(L, lane, k0, k1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    K::seg_chain_full(L, H, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
@@ -54,23 +54,23 @@ __global__ __launch_bounds__(256) void micro(int H, int reps, unsigned long long
     if (threadIdx.x >= 64) return;   // wave 0 only
     const int lane = threadIdx.x;
     init_data<ID>(L, H, lane, blockIdx.x & 7);
-    const int SM = K::seg_split(H);
+    const int S1 = K::seg_start(1, H), SL = K::seg_start(K::NSEG - 1, H);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     bool ok = true;
     for (int r = 0; r < reps; ++r) {
-        if constexpr (V == 0) ok = K::template seg_factor<true>(L, H, lane, 0, SM) && ok;
-        if constexpr (V == 1) ok = K::template seg_factor<false>(L, H, lane, SM, H) && ok;
-        if constexpr (V == 2) K::seg_boundary_full(L, H, lane);
+        if constexpr (V == 0) ok = K::template seg_factor<true>(L, H, lane, 0, S1, L.sb + K::SB_V) && ok;
+        if constexpr (V == 1) ok = K::template seg_factor<false>(L, H, lane, SL, H, nullptr) && ok;
+        if constexpr (V == 2) K::seg_chain_full(L, H, lane);
         if constexpr (V == 3) {
-            K::seg_fold(L, H, lane);
+            K::seg_fold(L, lane, 0, S1, L.sb + K::SB_LAM);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            K::seg_forward(L, lane, 0, SM, nullptr, false);
+            K::seg_forward(L, lane, 0, S1, nullptr, false);
         }
-        if constexpr (V == 4) K::seg_forward(L, lane, SM, H, L.sb + K::SB_XM, true);
-        if constexpr (V == 5) K::seg_vector_backward(L, H, lane, 0, SM, false);
-        if constexpr (V == 6) K::seg_vector_backward(L, H, lane, SM, H, true);
-        if constexpr (V == 7) K::seg_boundary_vec(L, H, lane);
-        if constexpr (V == 8) K::template seg_acl<true>(L, lane, 0, SM);
+        if constexpr (V == 4) K::seg_forward(L, lane, SL, H, L.sb + K::SB_XM + 8 * (K::NSEG - 1), true);
+        if constexpr (V == 5) K::seg_vector_backward(L, H, lane, 0, S1, false, L.sb + K::SB_VL1);
+        if constexpr (V == 6) K::seg_vector_backward(L, H, lane, SL, H, true, nullptr);
+        if constexpr (V == 7) K::seg_chain_vec(L, H, lane);
+        if constexpr (V == 8) K::template seg_acl<true>(L, lane, 0, S1);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -100,15 +100,15 @@ int main() {
     (void)hipMalloc(&d_out, B * sizeof(unsigned long long));
     (void)hipMalloc(&d_sink, B * 8 * sizeof(double));
     for (int H : {30}) {
-        run<kQuad2D, 0>("quad2d factor A (lambda, 15 stages)", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 1>("quad2d factor B (15 stages)", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 8>("quad2d acl<true> A", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 2>("quad2d boundary (predictor, GJ)", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 3>("quad2d fold + forward A", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 4>("quad2d forward B", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 5>("quad2d vector backward A (+ V_l1)", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 6>("quad2d vector backward B", H, B, reps, d_out, d_sink);
-        run<kQuad2D, 7>("quad2d boundary (corrector)", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 0>("quad2d factor first segment (lambda)", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 1>("quad2d factor last segment", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 8>("quad2d acl<true> first segment", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 2>("quad2d boundary chain (predictor)", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 3>("quad2d fold + forward first segment", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 4>("quad2d forward last segment", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 5>("quad2d vector backward first (+ V_l1)", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 6>("quad2d vector backward last", H, B, reps, d_out, d_sink);
+        run<kQuad2D, 7>("quad2d boundary chain (corrector)", H, B, reps, d_out, d_sink);
     }
     return 0;
 }
