@@ -1867,6 +1867,7 @@ struct SqpKernel {
                 WSYNC();
             }
         }
+        WSYNC();   // y_b, Y_b of every boundary before the forward pass reads them on other lanes
         seg_chain_forward(L, lane);
     }
 
