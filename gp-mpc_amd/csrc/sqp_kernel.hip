@@ -337,7 +337,9 @@ struct SqpKernel {
     // per segment its start state x_w
     static constexpr int SB_V = 0, SB_LAM = SB_V + 256 * NBD, SB_XM = SB_LAM + 8 * NBD, SB_VL1 = SB_XM + 8 * NSEG,
                          SB_TI = SB_VL1 + 8 * NBD, SB_Y = SB_TI + NX * NX * NBD, SB_YV = SB_Y + NX * NX * NBD,
-                         SB_PH = SB_YV + 8 * NBD, SB = SEG ? SB_PH + PP * NBD : 0;
+                         SB_PH = SB_YV + 8 * NBD, SB = SEG ? (SB_PH + PP * NBD + 7) / 8 * 8 : 0;
+    // (SB rounds up to 64 bytes: the regions carved after it keep the 16-byte alignment their wide
+    // LDS accesses assume)
 
     // LDS carve (doubles), sized by H at launch.
     struct Lds {
@@ -1868,13 +1870,14 @@ struct SqpKernel {
             }
         }
         WSYNC();   // y_b, Y_b of every boundary before the forward pass reads them on other lanes
-        seg_chain_forward(L, lane);
+        seg_chain_forward(L, lane, false);
     }
 
     // Forward over the boundaries from x_0 = 0: lambda_b = Y_b x_b + y_b (boundary 0: y_0),
     // x_{b+1} = V_lx x_b + V_l1 + V_ll lambda_b; lambda_b and the segment start states x_w into the
-    // boundary data.
-    __device__ static void seg_chain_forward(const Lds& L, int lane) {
+    // boundary data.  V_l1 is the tile's affine column after a factorisation, the corrector's vector
+    // pass result (SB_VL1) after a vector pass (vec).
+    __device__ static void seg_chain_forward(const Lds& L, int lane, bool vec) {
         constexpr int CI = NX;
         const int i = min(lane, NX - 1);
         double xh[NX];
@@ -1890,7 +1893,7 @@ struct SqpKernel {
             double lam[NX];
 #pragma unroll
             for (int j = 0; j < NX; ++j) lam[j] = readlane_d(lv, j);
-            double xn = V[(LI + i) * 16 + CI];
+            double xn = vec ? L.sb[SB_VL1 + 8 * b + i] : V[(LI + i) * 16 + CI];
 #pragma unroll
             for (int l = 0; l < NX; ++l) xn = fma(V[(LI + i) * 16 + l], xh[l], xn);
 #pragma unroll
@@ -1936,7 +1939,7 @@ struct SqpKernel {
             }
         }
         WSYNC();
-        seg_chain_forward(L, lane);
+        seg_chain_forward(L, lane, true);
     }
 
     // A segment with its solved terminal costate lambda: the feedforward kff_k += K_lambda,k lambda and
