@@ -1802,11 +1802,13 @@ struct SqpKernel {
             double pk[PP];
 #pragma unroll
             for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
+            // the lane's right-hand side column of the tile, loaded unconditionally (a load under a lane
+            // condition becomes a branch with its own wait)
+            const int bc = c < NX ? LI + c : (c < 2 * NX ? c - NX : CI);
+            const double bs = c < NX ? -1.0 : (c <= 2 * NX ? 1.0 : 0.0);
             double bv[NX];
 #pragma unroll
-            for (int l = 0; l < NX; ++l)
-                bv[l] = c < NX ? -V[(LI + l) * 16 + LI + c]
-                               : (c < 2 * NX ? V[(LI + l) * 16 + (c - NX)] : (c == 2 * NX ? V[(LI + l) * 16 + CI] : 0.0));
+            for (int l = 0; l < NX; ++l) bv[l] = bs * V[(LI + l) * 16 + bc];
             double col[NX];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
@@ -1839,32 +1841,31 @@ struct SqpKernel {
                 for (int i = 0; i < NX; ++i)
                     if (i != p) col[i] = fma(-cp[i], col[p], col[i]);
             }
-            if (lane >= NX && lane < 2 * NX) {
-                if (b >= 1) {
+            // branch-free stores: Y_b columns (b >= 1), y_b, T_b^-1 columns; other lanes into the dummy slots
+            {
+                const bool sy = b >= 1 && lane >= NX && lane < 2 * NX, syv = lane == 2 * NX,
+                           sti = lane > 2 * NX && lane <= 3 * NX;
+                double* dst = sy ? L.sb + SB_Y + b * NX * NX + (lane - NX)
+                                 : (syv ? L.sb + SB_YV + 8 * b
+                                        : (sti ? L.sb + SB_TI + b * NX * NX + (lane - 2 * NX - 1) : L.dummy + lane));
+                const int ds = (sy || sti) ? NX : (syv ? 1 : 0);
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) L.sb[SB_Y + b * NX * NX + i * NX + (lane - NX)] = col[i];
-                }
-            } else if (lane == 2 * NX) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) L.sb[SB_YV + 8 * b + i] = col[i];
-            } else if (lane > 2 * NX && lane <= 3 * NX) {
-#pragma unroll
-                for (int i = 0; i < NX; ++i) L.sb[SB_TI + b * NX * NX + i * NX + (lane - 2 * NX - 1)] = col[i];
+                for (int i = 0; i < NX; ++i) dst[i * ds] = col[i];
             }
             if (b >= 1) {
                 // cost-to-go at s_b, packed: lane NX + j (j < NX) column j of V_xx + V_xl Y_b, lane 2 NX the
-                // vector V_x1 + V_xl y_b
-                if (lane >= NX && lane <= 2 * NX) {
-                    const int j = lane - NX;
-                    double* dst = L.sb + SB_PH + (b - 1) * PP;
+                // vector V_x1 + V_xl y_b (tile loads unconditional, stores branch-free)
+                const int j = min(max(lane - NX, 0), NX);
+                const bool on = lane >= NX && lane <= 2 * NX;
+                double* dst = L.sb + SB_PH + (b - 1) * PP;
 #pragma unroll
-                    for (int i = 0; i < NX; ++i) {
-                        double acc = V[i * 16 + (j < NX ? j : CI)];
+                for (int i = 0; i < NX; ++i) {
+                    double acc = V[i * 16 + (j < NX ? j : CI)];
 #pragma unroll
-                        for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], col[l], acc);
-                        if (j == NX) dst[PO + i] = acc;
-                        else if (i <= j) dst[pidx(i, j)] = acc;
-                    }
+                    for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], col[l], acc);
+                    const bool st = on && (j == NX || i <= j);
+                    double* a = st ? dst + (j == NX ? PO + i : pidx(min(i, j), max(i, j))) : L.dummy + lane;
+                    *a = acc;
                 }
                 WSYNC();
             }
@@ -1898,9 +1899,10 @@ struct SqpKernel {
             for (int l = 0; l < NX; ++l) xn = fma(V[(LI + i) * 16 + l], xh[l], xn);
 #pragma unroll
             for (int j = 0; j < NX; ++j) xn = fma(V[(LI + i) * 16 + LI + j], lam[j], xn);
-            if (lane < NX) {
-                L.sb[SB_LAM + 8 * b + lane] = lv;
-                L.sb[SB_XM + 8 * (b + 1) + lane] = xn;
+            {
+                const bool st = lane < NX;
+                *(st ? L.sb + SB_LAM + 8 * b + lane : L.dummy + lane) = lv;
+                *(st ? L.sb + SB_XM + 8 * (b + 1) + lane : L.dummy + lane) = xn;
             }
 #pragma unroll
             for (int l = 0; l < NX; ++l) xh[l] = readlane_d(xn, l);
@@ -1926,7 +1928,7 @@ struct SqpKernel {
             double yv = 0.0;
 #pragma unroll
             for (int j = 0; j < NX; ++j) yv = fma(L.sb[SB_TI + b * NX * NX + i * NX + j], rv[j], yv);
-            if (lane < NX) L.sb[SB_YV + 8 * b + lane] = yv;
+            *(lane < NX ? L.sb + SB_YV + 8 * b + lane : L.dummy + lane) = yv;
             if (b >= 1) {
                 const double* V = L.sb + SB_V + b * 256;
                 double yu[NX];
