@@ -1853,20 +1853,18 @@ struct SqpKernel {
                 for (int i = 0; i < NX; ++i) dst[i * ds] = col[i];
             }
             if (b >= 1) {
-                // cost-to-go at s_b, packed: lane NX + j (j < NX) column j of V_xx + V_xl Y_b, lane 2 NX the
-                // vector V_x1 + V_xl y_b (tile loads unconditional, stores branch-free)
-                const int j = min(max(lane - NX, 0), NX);
-                const bool on = lane >= NX && lane <= 2 * NX;
-                double* dst = L.sb + SB_PH + (b - 1) * PP;
+                // cost-to-go at s_b, packed, one entry per lane: lane (i, j) = i (NX + 1) + j forms row i of
+                // column j of V_xx + V_xl Y_b (j < NX) or of the vector V_x1 + V_xl y_b (j = NX), from the
+                // Y_b / y_b just stored (one load round trip, stores branch-free)
+                WSYNC();
+                const int e = min(lane, NX * (NX + 1) - 1), i = e / (NX + 1), j = e - i * (NX + 1);
+                const double* yc = j < NX ? L.sb + SB_Y + b * NX * NX + j : L.sb + SB_YV + 8 * b;
+                const int ys = j < NX ? NX : 1;
+                double acc = V[i * 16 + (j < NX ? j : CI)];
 #pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double acc = V[i * 16 + (j < NX ? j : CI)];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], col[l], acc);
-                    const bool st = on && (j == NX || i <= j);
-                    double* a = st ? dst + (j == NX ? PO + i : pidx(min(i, j), max(i, j))) : L.dummy + lane;
-                    *a = acc;
-                }
+                for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], yc[l * ys], acc);
+                const bool st = lane < NX * (NX + 1) && (j == NX || i <= j);
+                *(st ? L.sb + SB_PH + (b - 1) * PP + (j == NX ? PO + i : pidx(min(i, j), max(i, j))) : L.dummy + lane) = acc;
                 WSYNC();
             }
         }
@@ -1884,7 +1882,9 @@ struct SqpKernel {
         double xh[NX];
 #pragma unroll
         for (int l = 0; l < NX; ++l) xh[l] = 0.0;
-        for (int b = 0; b < NSEG - 1; ++b) {
+        double lvs[NBD], xns[NBD];   // stored after the recursion, so every load can issue up front
+#pragma unroll
+        for (int b = 0; b < NBD; ++b) {
             const double* V = L.sb + SB_V + b * 256;
             double lv = L.sb[SB_YV + 8 * b + i];
             if (b >= 1) {
@@ -1899,13 +1899,18 @@ struct SqpKernel {
             for (int l = 0; l < NX; ++l) xn = fma(V[(LI + i) * 16 + l], xh[l], xn);
 #pragma unroll
             for (int j = 0; j < NX; ++j) xn = fma(V[(LI + i) * 16 + LI + j], lam[j], xn);
-            {
-                const bool st = lane < NX;
-                *(st ? L.sb + SB_LAM + 8 * b + lane : L.dummy + lane) = lv;
-                *(st ? L.sb + SB_XM + 8 * (b + 1) + lane : L.dummy + lane) = xn;
-            }
+            lvs[b] = lv;
+            xns[b] = xn;
+            if (b + 1 < NBD) {
 #pragma unroll
-            for (int l = 0; l < NX; ++l) xh[l] = readlane_d(xn, l);
+                for (int l = 0; l < NX; ++l) xh[l] = readlane_d(xn, l);
+            }
+        }
+        const bool st = lane < NX;
+#pragma unroll
+        for (int b = 0; b < NBD; ++b) {
+            *(st ? L.sb + SB_LAM + 8 * b + lane : L.dummy + lane) = lvs[b];
+            *(st ? L.sb + SB_XM + 8 * (b + 1) + lane : L.dummy + lane) = xns[b];
         }
         WSYNC();
     }
@@ -1917,8 +1922,10 @@ struct SqpKernel {
     __device__ static void seg_chain_vec(const Lds& L, int H, int lane) {
         const int i = min(lane, NX - 1);
         double phv = L.P[(size_t)seg_start(NSEG - 1, H) * PPB + PO + i];
-        for (int b = NSEG - 2; b >= 0; --b) {
-            const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
+        double yvs[NBD];   // stored after the recursion, so every load can issue up front
+#pragma unroll
+        for (int b = NBD - 1; b >= 0; --b) {
+            const double* Pm = (b == NBD - 1) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
             double r = phv;
 #pragma unroll
             for (int l = 0; l < NX; ++l) r = fma(Pm[i <= l ? pidx(i, l) : pidx(l, i)], L.sb[SB_VL1 + 8 * b + l], r);
@@ -1928,7 +1935,7 @@ struct SqpKernel {
             double yv = 0.0;
 #pragma unroll
             for (int j = 0; j < NX; ++j) yv = fma(L.sb[SB_TI + b * NX * NX + i * NX + j], rv[j], yv);
-            *(lane < NX ? L.sb + SB_YV + 8 * b + lane : L.dummy + lane) = yv;
+            yvs[b] = yv;
             if (b >= 1) {
                 const double* V = L.sb + SB_V + b * 256;
                 double yu[NX];
@@ -1940,6 +1947,8 @@ struct SqpKernel {
                 phv = p1;
             }
         }
+#pragma unroll
+        for (int b = 0; b < NBD; ++b) *(lane < NX ? L.sb + SB_YV + 8 * b + lane : L.dummy + lane) = yvs[b];
         WSYNC();
         seg_chain_forward(L, lane, true);
     }
