@@ -146,6 +146,11 @@ __device__ __forceinline__ f64x4 mfma64(double a, double b, f64x4 c) {
 // |eps| <= 2^-23, refined by one cubic step r0 (1 + e + e^2), e = 1 - x r0, whose error is eps^3.
 // Three dependent f64 ops after the estimate instead of four for two Newton steps (a dependent
 // f64 VALU op waits ~7.3 cycles on gfx950, tools/probe_f64.hip).
+// |x| ordering key: the high word with the sign cleared (exponent and 20 mantissa bits)
+__device__ __forceinline__ unsigned hi_abs(double x) {
+    return (unsigned)((unsigned long long)__double_as_longlong(x) >> 32) & 0x7fffffffu;
+}
+
 __device__ __forceinline__ double fast_rcp(double x) {
     const double r = __builtin_amdgcn_rcp(x);
     const double e = fma(-x, r, 1.0);
@@ -1757,20 +1762,28 @@ struct SqpKernel {
         }
         WSYNC();
         if (!last) {
-            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k with z_k = c_k + B_k kff_k, the affine column of the
-            // closed-loop map A'_k (seg_acl<false> with this pass's kff): lane (k, j) forms term j of
-            // stage k into VT (its p-recurrence input is consumed), then lanes j < NX add the terms
-            seg_acl<false>(L, lane, k0, k1);
-            WSYNC();
+            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k with z_k = c_k + B_k kff_k (this pass's kff, formed
+            // here: the closed-loop maps' affine columns follow during the chain, seg_part): lane (k, j)
+            // forms term j of stage k into VT (its p-recurrence input is consumed), then lanes j < NX add
+            // the terms
             for (int e = k0 * NX + lane; e < n; e += 64) {
                 const int k = e / NX, j = e - k * NX;
-                const double* Ak = L.Acl + (size_t)k * NX * PS + NX;
+                const double* G = L.G + (size_t)k * NX * GS;
+                const double* Kk = L.K + (size_t)k * NU * KST + NX;
                 const double* Pl = L.P + (size_t)(k + 1) * PPB + PXL;
+                double kf[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) kf[a] = Kk[a * KST];
+                // P_lambda,x,k1 = I at the segment end; the P' load stays unconditional (bsel), a ternary
+                // would sink it into a branch with a wait per term
+                const unsigned mend = (k + 1 == k1) ? 0xffffffffu : 0u;
                 double acc = 0.0;
 #pragma unroll
                 for (int t = 0; t < NX; ++t) {
-                    const double z = Ak[t * PS];
-                    acc = (k + 1 == k1) ? (t == j ? z : acc) : fma(Pl[t * NX + j], z, acc);
+                    double z = G[t * GS + NB];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) z = fma(G[t * GS + NX + a], kf[a], z);
+                    acc = fma(bsel(mend, t == j ? 1.0 : 0.0, Pl[t * NX + j]), z, acc);
                 }
                 VT[e] = acc;
             }
@@ -1823,11 +1836,17 @@ struct SqpKernel {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
+                // pivot: the largest |T_ip| (i >= p) compared on the high words (sign cleared: exponent and
+                // 20 mantissa bits), integer work on the uniform read-lane values, so the choice and the
+                // swaps below stay scalar
                 int piv = p;
-                double best = fabs(cp[p]);
+                unsigned best = hi_abs(cp[p]);
 #pragma unroll
-                for (int i = p + 1; i < NX; ++i)
-                    if (fabs(cp[i]) > best) { best = fabs(cp[i]); piv = i; }
+                for (int i = p + 1; i < NX; ++i) {
+                    const unsigned h = hi_abs(cp[i]);
+                    piv = h > best ? i : piv;
+                    best = h > best ? h : best;
+                }
 #pragma unroll
                 for (int i = p + 1; i < NX; ++i) {
                     if (piv == i) {
@@ -1981,9 +2000,12 @@ struct SqpKernel {
             double pv = Pk[PO + i];
 #pragma unroll
             for (int j = 0; j < NX; ++j) pv = fma(Pk[PXL + i * NX + j], lam[j], pv);
+            // every load before the first store, stores branch-free (dummy slots for the other lanes)
+            double* kp = i < NU ? L.K + (size_t)k * NU * KST + min(i, NU - 1) * KST + NX : L.dummy + lane;
+            const double kv = *kp;
             L.Acl[(size_t)k * NX * PS + i * PS + NX] = ac;
-            if (k >= 1) Pk[PO + i] = pv;
-            if (i < NU) L.K[(size_t)k * NU * KST + i * KST + NX] += dk[i < NU ? i : 0];
+            *(k >= 1 ? Pk + PO + i : L.dummy + lane) = pv;
+            *kp = kv + dk[i < NU ? i : 0];
         }
     }
 
@@ -2028,35 +2050,47 @@ struct SqpKernel {
     // -- only posts and waits; waves 1 and 0 with two (wave 0 then runs the last segment, an ordinary
     // recursion over a range: no more registers than the one-segment kernel's).  Wave 1 also runs the
     // boundary chain.
-    //   kCmdSegFactor (predictor): B1 | factorisations + closed-loop maps | Bm1 | wave 1: chain | Bm2 |
-    //                 forward sweeps (after the fold of each segment's lambda) | B2
-    //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain | Bm2 | forward | B2
+    //   kCmdSegFactor (predictor): B1 | factorisations | Bm1 | wave 1: chain, others: closed-loop maps |
+    //                 Bm2 | forward sweeps (after the fold of each segment's lambda) | B2
+    //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain, others: affine columns |
+    //                 Bm2 | forward | B2
     // Factorisation statuses in ctrl[8 + w].
     static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
     __host__ __device__ static constexpr int seg_of_wave(int w) { return NSEG == 3 ? w - 1 : (w == 1 ? 0 : (w == 0 ? 1 : -1)); }
     // KIND 0: no segment on this wave; 1: segment sg < NSEG - 1 (lambda recursion); 2: the last segment
+    // The closed-loop maps A'_k (seg_acl) are formed between Bm1 and Bm2, while wave 1 runs the boundary
+    // chain, by the waves free then: with three segments wave 2 those of segments 0 and 1 and wave 3 the
+    // last segment's (wave 0, holding the IPM state, takes none); with two, wave 0 all of them.
+    __device__ static void acl_range(int w, int H, int& a0, int& a1) {
+        if constexpr (NSEG == 3) {
+            a0 = w == 3 ? seg_start(2, H) : 0;
+            a1 = w == 2 ? seg_start(2, H) : (w == 3 ? H : 0);
+        } else {
+            a0 = 0;
+            a1 = w == 0 ? H : 0;
+        }
+    }
     template <int KIND>
-    __device__ static bool seg_part(const Lds& L, int H, int lane, int sg, bool chain, int cmd) {
+    __device__ static bool seg_part(const Lds& L, int H, int lane, int w, int sg, bool chain, int cmd) {
         const int k0 = seg_start(sg, H), k1 = seg_start(sg + 1, H);
         double* xs = L.sb + SB_XM + 8 * sg;
+        int a0, a1;
+        acl_range(w, H, a0, a1);
         bool ok = true;
         if (cmd == kCmdSegFactor) {
             if constexpr (KIND == 1) {
                 const bool fok = seg_factor<true>(L, H, lane, k0, k1, L.sb + SB_V + sg * 256);
-                WSYNC();
-                seg_acl<true>(L, lane, k0, k1);
                 if (lane == 0) L.ctrl[8 + sg] = fok ? 1 : 0;
             } else if constexpr (KIND == 2) {
                 const bool fok = seg_factor<false>(L, H, lane, k0, H, nullptr);
-                WSYNC();
-                seg_acl<true>(L, lane, k0, H);
                 if (lane == 0) L.ctrl[8 + sg] = fok ? 1 : 0;
             }
             __syncthreads();   // Bm1
 #pragma unroll
             for (int q = 0; q < NSEG; ++q) ok = ok && L.ctrl[8 + q] != 0;
             if (chain && ok) seg_chain_full(L, H, lane);
-            __syncthreads();   // Bm2: lambda_b, x_w
+            if (a1 > a0) seg_acl<true>(L, lane, a0, a1);
+            __syncthreads();   // Bm2: lambda_b, x_w, A'_k
             if (ok) {
                 if constexpr (KIND == 1) {
                     seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
@@ -2072,14 +2106,13 @@ struct SqpKernel {
             if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
             __syncthreads();   // Bm1
             if (chain) seg_chain_vec(L, H, lane);
-            __syncthreads();   // Bm2: lambda_b, x_w
+            if (a1 > a0) seg_acl<false>(L, lane, a0, a1);
+            __syncthreads();   // Bm2: lambda_b, x_w, A'_k[:, CI]
             if constexpr (KIND == 1) {
                 seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
                 WSYNC();
                 seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
             } else if constexpr (KIND == 2) {
-                seg_acl<false>(L, lane, k0, H);
-                WSYNC();
                 seg_forward(L, lane, k0, H, xs, true);
             }
             __syncthreads();   // B2
@@ -2091,14 +2124,14 @@ struct SqpKernel {
         if (lane == 0) L.ctrl[0] = cmd;
         __syncthreads();   // B1
         constexpr int sg0 = seg_of_wave(0);
-        return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, sg0 < 0 ? 0 : sg0, false, cmd);
+        return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd);
     }
     // helper wave w's part of a segment command (after B1)
     __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
         const int sg = seg_of_wave(w);
-        if (sg == NSEG - 1) (void)seg_part<2>(L, H, lane, sg, w == 1, cmd);
-        else if (sg >= 0) (void)seg_part<1>(L, H, lane, sg, w == 1, cmd);
-        else (void)seg_part<0>(L, H, lane, 0, false, cmd);
+        if (sg == NSEG - 1) (void)seg_part<2>(L, H, lane, w, sg, w == 1, cmd);
+        else if (sg >= 0) (void)seg_part<1>(L, H, lane, w, sg, w == 1, cmd);
+        else (void)seg_part<0>(L, H, lane, w, 0, false, cmd);
     }
 
     // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
