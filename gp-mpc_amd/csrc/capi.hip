@@ -831,6 +831,14 @@ gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* wave
     return GPMPC_OK;
 }
 
+gpmpc_status gpmpc_get_launch_segments(gpmpc_handle* h, int32_t batch, int32_t* segments) {
+    if (!h) return fail(GPMPC_ERR_ARG, "null handle");
+    if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
+    if (!segments) return fail(GPMPC_ERR_ARG, "null output");
+    *segments = sqp_launch_segments(h->P, batch);
+    return GPMPC_OK;
+}
+
 gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value) {
     if (!h) return fail(GPMPC_ERR_ARG, "null handle");
     switch (option) {

@@ -245,6 +245,7 @@ hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, 
 hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream);
 bool sqp_overlap_ok(const ProblemDev& P, int batch);
 int sqp_launch_waves(const ProblemDev& P, int batch);   // waves per instance launch_sqp would use
+int sqp_launch_segments(const ProblemDev& P, int batch);   // horizon segments of its Newton solves
 size_t sqp_lds_bytes(int model, int H);
 int model_unc_dims(int model, int32_t* unc);   // the model's uncertain state dims (Bd columns), returns their count
 hipError_t launch_stage_cost(const ProblemDev& P, const double* x, const double* u, const int32_t* tstep,

@@ -3326,6 +3326,23 @@ int sqp_launch_waves(const ProblemDev& P, int batch) {
     }
     return 0;
 }
+template <int ID>
+static int segments_of(const ProblemDev& P, int batch) {
+    if constexpr (kDefaultWaves<ID> == 1) {
+        const int nw = sqp_waves<ID>(P, batch);
+        if (!sqp_seg_of(P, nw)) return 1;
+        return nw == 4 ? SqpKernel<ID, 4, true>::NSEG : SqpKernel<ID, 2, true>::NSEG;
+    }
+    return 1;
+}
+int sqp_launch_segments(const ProblemDev& P, int batch) {
+    switch (P.model) {
+        case kQuad2D: return segments_of<kQuad2D>(P, batch);
+        case kQuad3D: return segments_of<kQuad3D>(P, batch);
+        case kCartpole: return segments_of<kCartpole>(P, batch);
+    }
+    return 0;
+}
 
 // order[] = the instances by decreasing cost of their last solve
 hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream) {

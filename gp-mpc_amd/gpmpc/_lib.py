@@ -52,6 +52,7 @@ SIGNATURES = {
     "gpmpc_get_variance": (_I, [_P, _I, _P, _P]),
     "gpmpc_lds_bytes": (c_int64, [_I, _I]),
     "gpmpc_get_launch_info": (_I, [_P, _I, POINTER(_I), POINTER(_I)]),
+    "gpmpc_get_launch_segments": (_I, [_P, _I, POINTER(_I)]),
     "gpmpc_set_tuning": (_I, [_P, _I, _I]),
     "gpmpc_set_cost_buffer": (_I, [_P, _P]),
 }

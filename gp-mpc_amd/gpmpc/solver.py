@@ -203,12 +203,14 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_launch(self._h, int(waves)))
 
     def launch_info(self) -> dict:
-        """What a solve of this batch runs (gpmpc_get_launch_info): SQP waves per instance, and
-        whether a step with a variance launch runs as overlapped halves (then the profiling events
-        bracket spans of the step, not single kernels)."""
-        w, o = ctypes.c_int32(), ctypes.c_int32()
+        """What a solve of this batch runs (gpmpc_get_launch_info, gpmpc_get_launch_segments): SQP
+        waves per instance, horizon segments of its Newton solves, and whether a step with a variance
+        launch runs as overlapped halves (then the profiling events bracket spans of the step, not
+        single kernels)."""
+        w, o, g = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self.lib.gpmpc_get_launch_info(self._h, self.batch, ctypes.byref(w), ctypes.byref(o)))
-        return {"waves": w.value, "overlapped": bool(o.value)}
+        _lib.check(self.lib.gpmpc_get_launch_segments(self._h, self.batch, ctypes.byref(g)))
+        return {"waves": w.value, "segments": g.value, "overlapped": bool(o.value)}
 
     def set_tuning(self, **opts):
         """Performance switches (gpmpc_set_tuning): lin_cache=0/1, order=0/1/2, overlap=0/1,

@@ -201,6 +201,11 @@ gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves);
  * cheaper half's variance launch): spans of the step, not per-kernel durations. */
 gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* waves, int32_t* overlapped);
 
+/* Horizon segments of the Newton solves gpmpc_solve would run for `batch` instances (host, no
+ * device work): 1 = one wave runs each recursion over the whole horizon; 2 or 3 = the
+ * segment-parallel solve of GPMPC_TUNE_SEG (two segments on two waves per instance, three on four). */
+gpmpc_status gpmpc_get_launch_segments(gpmpc_handle* h, int32_t batch, int32_t* segments);
+
 /* Performance switches (no reference counterpart; every output is bit-identical or identical up
  * to rounding whichever value is set -- A/B measurement knobs, all on their default after
  * gpmpc_create).  gpmpc_set_tuning(h, option, value):
@@ -214,9 +219,10 @@ gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* wave
  *                          triangular variance kernel; 4: its four-wave column split
  *   GPMPC_TUNE_EVENT_FENCE 0 (default): profiling events without the system-scope fence;
  *                          1: default (fenced) events
- *   GPMPC_TUNE_SEG         1 (default): two-segment Newton solves when a launch runs two or four
- *                          waves per instance (quad2d, cartpole): the horizon's two halves are
- *                          factorised and swept on two waves at once and joined at the boundary;
+ *   GPMPC_TUNE_SEG         1 (default): segment-parallel Newton solves when a launch runs two or
+ *                          four waves per instance (quad2d, cartpole): the horizon's two (two
+ *                          waves) or three (four waves) segments are factorised and swept on
+ *                          different waves at once and joined by a chain over the boundaries;
  *                          0: one wave runs the whole recursion; identical up to rounding */
 enum {
     GPMPC_TUNE_LIN_CACHE = 0,

@@ -106,6 +106,27 @@ def test_launch_option_validation():
     q3.set_launch(waves=0)
 
 
+def test_launch_segments_follow_waves_and_tuning():
+    """gpmpc_get_launch_segments: three horizon segments on four waves, two on two, one with the
+    segment solve off, on one wave, or for quad3d."""
+    _torch()
+    from gpmpc.models import get_spec
+    from gpmpc.solver import BatchSolver
+
+    spec, _, _ = problem("quad2d", 20)
+    gs = BatchSolver(spec, 30, 2)
+    for waves, seg, want in ((4, 1, 3), (2, 1, 2), (1, 1, 1), (4, 0, 1), (2, 0, 1)):
+        gs.set_launch(waves=waves)
+        gs.set_tuning(seg=seg)
+        info = gs.launch_info()
+        assert info["waves"] == waves and info["segments"] == want, (waves, seg, info)
+    gs.set_launch(waves=0)
+    gs.set_tuning(seg=1)
+    assert gs.launch_info() == {"waves": 4, "segments": 3, "overlapped": False}   # 2 instances <= CUs
+    q3 = BatchSolver(get_spec("quad3d"), 10, 2)
+    assert q3.launch_info()["segments"] == 1
+
+
 def test_cost_ordered_dispatch_is_bit_exact():
     """A launch with more instances than the device holds at once (quad3d: one instance per CU)
     dispatches them by decreasing previous-solve cost (StateDev::order); which CU runs an instance
