@@ -225,8 +225,11 @@ def parse_args(argv=None):
                          "NLP tolerances on to the QP solver)")
     ap.add_argument("--qp-mu0", type=float, default=1.0)
     ap.add_argument("--seg", type=int, choices=[0, 1], default=None,
-                    help="two-segment Newton solves on launches with two or four waves per instance "
+                    help="segment-parallel Newton solves on launches with two or four waves per instance "
                          "(gpmpc_set_tuning GPMPC_TUNE_SEG; default: the library's)")
+    ap.add_argument("--overlap", type=int, choices=[0, 1], default=None,
+                    help="overlapped halves for steps needing more than one round of workgroups "
+                         "(gpmpc_set_tuning GPMPC_TUNE_OVERLAP; default: the library's)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
@@ -396,6 +399,8 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         solver = BatchSolver(spec, H, B, device=dev, qp_tol=args.qp_tol, qp_mu0=args.qp_mu0)
         if args.seg is not None:
             solver.set_tuning(seg=args.seg)
+        if args.overlap is not None:
+            solver.set_tuning(overlap=args.overlap)
         solver.set_gps(gps, fitc=fitc, variance=args.variance)
         solver.set_tightening(True, 0.95, *lqr_mats)
         solver.reset(reset_iterate=True)
