@@ -1802,31 +1802,44 @@ struct SqpKernel {
     // true cost-to-go Ph, ph at s_{b+1} (the last segment's P' there, or the previous boundary's result):
     //   T_b = I - Ph V_ll,   [Y_b | y_b] = T_b^-1 [Ph V_lx | Ph V_l1 + ph],
     //   Ph <- V_xx + V_xl Y_b,  ph <- V_x1 + V_xl y_b          (the cost-to-go at s_b, for boundary b - 1)
-    // (lambda_b = Ph x_{b+1} + ph and x_{b+1} = V_lx x_b + V_l1 + V_ll lambda_b), by Gauss-Jordan with
-    // partial pivoting, lane c holding column c of [T | Ph V_lx | r | I] (rows in registers; the pivot
-    // column is read by v_readlane, so the pivot choice is uniform).  Then seg_chain_forward.  T_b^-1,
-    // Y_b and the computed cost-to-go matrices stay in the boundary data for the corrector.
+    // (lambda_b = Ph x_{b+1} + ph and x_{b+1} = V_lx x_b + V_l1 + V_ll lambda_b).  T_b is not symmetric,
+    // but with W = -V_ll (negative semidefinite: the segment's value is concave in its terminal costate)
+    //   T_b^-1 = Ph M^-1,   M = Ph + Ph W Ph   (symmetric positive definite: Ph > 0, W >= 0),
+    // so Gauss-Jordan runs on M without pivoting (no pivot search or row swaps on the chain's critical
+    // path), lane c holding column c of [M | Ph V_lx | Ph V_l1 + ph | I] (rows in registers, the pivot
+    // column read by v_readlane), and [Y_b | y_b | T_b^-1] = Ph x (the eliminated right-hand sides).
+    // Then seg_chain_forward.  T_b^-1, Y_b and the computed cost-to-go matrices stay in the boundary
+    // data for the corrector.
     __device__ static void seg_chain_full(const Lds& L, int H, int lane) {
         constexpr int CI = NX;
         const int c = min(lane, 3 * NX);
+        const int cm = min(c, NX - 1);
+        const unsigned mcol = c < NX ? 0xffffffffu : 0u;
         for (int b = NSEG - 2; b >= 0; --b) {
             const double* V = L.sb + SB_V + b * 256;
             const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
             double pk[PP];
 #pragma unroll
             for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
-            // the lane's right-hand side column of the tile, loaded unconditionally (a load under a lane
-            // condition becomes a branch with its own wait)
-            const int bc = c < NX ? LI + c : (c < 2 * NX ? c - NX : CI);
-            const double bs = c < NX ? -1.0 : (c <= 2 * NX ? 1.0 : 0.0);
+            // every load unconditional (a load under a lane condition becomes a branch with its own
+            // wait): column cm of Ph, the uniform V_ll, and the lane's right-hand side column of the tile
+            double phc[NX];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) phc[m] = Pm[m <= cm ? pidx(m, cm) : pidx(cm, m)];
+            const int bc = (c >= NX && c < 2 * NX) ? c - NX : CI;
+            const double bs = (c >= NX && c <= 2 * NX) ? 1.0 : 0.0;
             double bv[NX];
 #pragma unroll
-            for (int l = 0; l < NX; ++l) bv[l] = bs * V[(LI + l) * 16 + bc];
+            for (int l = 0; l < NX; ++l) {
+                double w = (l == cm) ? 1.0 : 0.0;   // (e_c + W Ph e_c)_l
+#pragma unroll
+                for (int m = 0; m < NX; ++m) w = fma(-V[(LI + l) * 16 + LI + m], phc[m], w);
+                bv[l] = bsel(mcol, w, bs * V[(LI + l) * 16 + bc]);
+            }
             double col[NX];
 #pragma unroll
             for (int i = 0; i < NX; ++i) {
-                double acc = c < NX ? (i == c ? 1.0 : 0.0)
-                                    : (c == 2 * NX ? pk[PO + i] : (c > 2 * NX ? (i == c - 2 * NX - 1 ? 1.0 : 0.0) : 0.0));
+                double acc = c == 2 * NX ? pk[PO + i] : (c > 2 * NX ? (i == c - 2 * NX - 1 ? 1.0 : 0.0) : 0.0);
 #pragma unroll
                 for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], bv[l], acc);
                 col[i] = acc;
@@ -1836,30 +1849,22 @@ struct SqpKernel {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
-                // pivot: the largest |T_ip| (i >= p) compared on the high words (sign cleared: exponent and
-                // 20 mantissa bits), integer work on the uniform read-lane values, so the choice and the
-                // swaps below stay scalar
-                int piv = p;
-                unsigned best = hi_abs(cp[p]);
-#pragma unroll
-                for (int i = p + 1; i < NX; ++i) {
-                    const unsigned h = hi_abs(cp[i]);
-                    piv = h > best ? i : piv;
-                    best = h > best ? h : best;
-                }
-#pragma unroll
-                for (int i = p + 1; i < NX; ++i) {
-                    if (piv == i) {
-                        const double t0 = col[p]; col[p] = col[i]; col[i] = t0;
-                        const double t1 = cp[p]; cp[p] = cp[i]; cp[i] = t1;
-                    }
-                }
                 const double inv = fast_rcp(cp[p]);
                 col[p] *= inv;
 #pragma unroll
                 for (int i = 0; i < NX; ++i)
                     if (i != p) col[i] = fma(-cp[i], col[p], col[i]);
             }
+            // [Y_b | y_b | T_b^-1] = Ph M^-1 [...]
+#pragma unroll
+            for (int i = 0; i < NX; ++i) {
+                double acc = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], col[l], acc);
+                bv[i] = acc;
+            }
+#pragma unroll
+            for (int i = 0; i < NX; ++i) col[i] = bv[i];
             // branch-free stores: Y_b columns (b >= 1), y_b, T_b^-1 columns; other lanes into the dummy slots
             {
                 const bool sy = b >= 1 && lane >= NX && lane < 2 * NX, syv = lane == 2 * NX,
