@@ -1818,23 +1818,30 @@ struct SqpKernel {
         for (int b = NSEG - 2; b >= 0; --b) {
             const double* V = L.sb + SB_V + b * 256;
             const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
-            double pk[PP];
-#pragma unroll
-            for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
-            // every load unconditional (a load under a lane condition becomes a branch with its own
-            // wait): column cm of Ph, the uniform V_ll, and the lane's right-hand side column of the tile
-            double phc[NX];
-#pragma unroll
-            for (int m = 0; m < NX; ++m) phc[m] = Pm[m <= cm ? pidx(m, cm) : pidx(cm, m)];
+            // every load first and unconditional (a load under a lane condition becomes a branch with its
+            // own wait; loads interleaved with their uses issue a few at a time): Ph, column cm of Ph, the
+            // uniform V_ll and the lane's right-hand side column of the tile
             const int bc = (c >= NX && c < 2 * NX) ? c - NX : CI;
             const double bs = (c >= NX && c <= 2 * NX) ? 1.0 : 0.0;
+            double pk[PP], phc[NX], vll[NX][NX], vr[NX];
+#pragma unroll
+            for (int q = 0; q < PP; ++q) pk[q] = Pm[q];
+#pragma unroll
+            for (int m = 0; m < NX; ++m) phc[m] = Pm[m <= cm ? pidx(m, cm) : pidx(cm, m)];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                vr[l] = V[(LI + l) * 16 + bc];
+#pragma unroll
+                for (int m = 0; m < NX; ++m) vll[l][m] = V[(LI + l) * 16 + LI + m];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keeps the scheduler from sinking the loads into their uses
             double bv[NX];
 #pragma unroll
             for (int l = 0; l < NX; ++l) {
                 double w = (l == cm) ? 1.0 : 0.0;   // (e_c + W Ph e_c)_l
 #pragma unroll
-                for (int m = 0; m < NX; ++m) w = fma(-V[(LI + l) * 16 + LI + m], phc[m], w);
-                bv[l] = bsel(mcol, w, bs * V[(LI + l) * 16 + bc]);
+                for (int m = 0; m < NX; ++m) w = fma(-vll[l][m], phc[m], w);
+                bv[l] = bsel(mcol, w, bs * vr[l]);
             }
             double col[NX];
 #pragma unroll
