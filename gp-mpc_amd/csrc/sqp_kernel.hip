@@ -1771,19 +1771,27 @@ struct SqpKernel {
                 const double* G = L.G + (size_t)k * NX * GS;
                 const double* Kk = L.K + (size_t)k * NU * KST + NX;
                 const double* Pl = L.P + (size_t)(k + 1) * PPB + PXL;
-                double kf[NU];
+                // every load first (before a scheduling barrier); P_lambda,x,k1 = I at the segment end, the
+                // P' load unconditional (bsel: a ternary would sink it into a branch with a wait per term)
+                double kf[NU], gc[NX], gu[NX][NU], pl[NX];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) kf[a] = Kk[a * KST];
-                // P_lambda,x,k1 = I at the segment end; the P' load stays unconditional (bsel), a ternary
-                // would sink it into a branch with a wait per term
+#pragma unroll
+                for (int t = 0; t < NX; ++t) {
+                    gc[t] = G[t * GS + NB];
+                    pl[t] = Pl[t * NX + j];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) gu[t][a] = G[t * GS + NX + a];
+                }
+                __builtin_amdgcn_sched_barrier(0);
                 const unsigned mend = (k + 1 == k1) ? 0xffffffffu : 0u;
                 double acc = 0.0;
 #pragma unroll
                 for (int t = 0; t < NX; ++t) {
-                    double z = G[t * GS + NB];
+                    double z = gc[t];
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) z = fma(G[t * GS + NX + a], kf[a], z);
-                    acc = fma(bsel(mend, t == j ? 1.0 : 0.0, Pl[t * NX + j]), z, acc);
+                    for (int a = 0; a < NU; ++a) z = fma(gu[t][a], kf[a], z);
+                    acc = fma(bsel(mend, t == j ? 1.0 : 0.0, pl[t]), z, acc);
                 }
                 VT[e] = acc;
             }
@@ -1891,9 +1899,15 @@ struct SqpKernel {
                 const int e = min(lane, NX * (NX + 1) - 1), i = e / (NX + 1), j = e - i * (NX + 1);
                 const double* yc = j < NX ? L.sb + SB_Y + b * NX * NX + j : L.sb + SB_YV + 8 * b;
                 const int ys = j < NX ? NX : 1;
-                double acc = V[i * 16 + (j < NX ? j : CI)];
+                double acc = V[i * 16 + (j < NX ? j : CI)], vxl[NX], yl[NX];
 #pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(V[i * 16 + LI + l], yc[l * ys], acc);
+                for (int l = 0; l < NX; ++l) {
+                    vxl[l] = V[i * 16 + LI + l];
+                    yl[l] = yc[l * ys];
+                }
+                __builtin_amdgcn_sched_barrier(0);   // loads first
+#pragma unroll
+                for (int l = 0; l < NX; ++l) acc = fma(vxl[l], yl[l], acc);
                 const bool st = lane < NX * (NX + 1) && (j == NX || i <= j);
                 *(st ? L.sb + SB_PH + (b - 1) * PP + (j == NX ? PO + i : pidx(min(i, j), max(i, j))) : L.dummy + lane) = acc;
                 WSYNC();
@@ -1913,23 +1927,37 @@ struct SqpKernel {
         double xh[NX];
 #pragma unroll
         for (int l = 0; l < NX; ++l) xh[l] = 0.0;
-        double lvs[NBD], xns[NBD];   // stored after the recursion, so every load can issue up front
+        // every load first (before a scheduling barrier), the stores after the recursion
+        double yv0[NBD], yr[NBD][NX], v1[NBD], vx[NBD][NX], vl[NBD][NX];
 #pragma unroll
         for (int b = 0; b < NBD; ++b) {
             const double* V = L.sb + SB_V + b * 256;
-            double lv = L.sb[SB_YV + 8 * b + i];
+            yv0[b] = L.sb[SB_YV + 8 * b + i];
+            v1[b] = vec ? L.sb[SB_VL1 + 8 * b + i] : V[(LI + i) * 16 + CI];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                yr[b][l] = b >= 1 ? L.sb[SB_Y + b * NX * NX + i * NX + l] : 0.0;
+                vx[b][l] = V[(LI + i) * 16 + l];
+                vl[b][l] = V[(LI + i) * 16 + LI + l];
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double lvs[NBD], xns[NBD];
+#pragma unroll
+        for (int b = 0; b < NBD; ++b) {
+            double lv = yv0[b];
             if (b >= 1) {
 #pragma unroll
-                for (int l = 0; l < NX; ++l) lv = fma(L.sb[SB_Y + b * NX * NX + i * NX + l], xh[l], lv);
+                for (int l = 0; l < NX; ++l) lv = fma(yr[b][l], xh[l], lv);
             }
             double lam[NX];
 #pragma unroll
             for (int j = 0; j < NX; ++j) lam[j] = readlane_d(lv, j);
-            double xn = vec ? L.sb[SB_VL1 + 8 * b + i] : V[(LI + i) * 16 + CI];
+            double xn = v1[b];
 #pragma unroll
-            for (int l = 0; l < NX; ++l) xn = fma(V[(LI + i) * 16 + l], xh[l], xn);
+            for (int l = 0; l < NX; ++l) xn = fma(vx[b][l], xh[l], xn);
 #pragma unroll
-            for (int j = 0; j < NX; ++j) xn = fma(V[(LI + i) * 16 + LI + j], lam[j], xn);
+            for (int j = 0; j < NX; ++j) xn = fma(vl[b][j], lam[j], xn);
             lvs[b] = lv;
             xns[b] = xn;
             if (b + 1 < NBD) {
@@ -1952,29 +1980,43 @@ struct SqpKernel {
     //   y_b = T_b^-1 (Ph V_l1 + ph),  ph <- V_x1 + V_xl y_b,  then seg_chain_forward.
     __device__ static void seg_chain_vec(const Lds& L, int H, int lane) {
         const int i = min(lane, NX - 1);
+        // every load first (before a scheduling barrier), the stores after the recursion
         double phv = L.P[(size_t)seg_start(NSEG - 1, H) * PPB + PO + i];
-        double yvs[NBD];   // stored after the recursion, so every load can issue up front
+        double prow[NBD][NX], vl1[NBD][NX], ti[NBD][NX], p1s[NBD], vxl[NBD][NX];
 #pragma unroll
         for (int b = NBD - 1; b >= 0; --b) {
             const double* Pm = (b == NBD - 1) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
+            const double* V = L.sb + SB_V + b * 256;
+            p1s[b] = b >= 1 ? L.P[(size_t)seg_start(b, H) * PPB + PO + i] : 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                prow[b][l] = Pm[i <= l ? pidx(i, l) : pidx(l, i)];
+                vl1[b][l] = L.sb[SB_VL1 + 8 * b + l];
+                ti[b][l] = L.sb[SB_TI + b * NX * NX + i * NX + l];
+                vxl[b][l] = b >= 1 ? V[i * 16 + LI + l] : 0.0;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double yvs[NBD];
+#pragma unroll
+        for (int b = NBD - 1; b >= 0; --b) {
             double r = phv;
 #pragma unroll
-            for (int l = 0; l < NX; ++l) r = fma(Pm[i <= l ? pidx(i, l) : pidx(l, i)], L.sb[SB_VL1 + 8 * b + l], r);
+            for (int l = 0; l < NX; ++l) r = fma(prow[b][l], vl1[b][l], r);
             double rv[NX];
 #pragma unroll
             for (int j = 0; j < NX; ++j) rv[j] = readlane_d(r, j);
             double yv = 0.0;
 #pragma unroll
-            for (int j = 0; j < NX; ++j) yv = fma(L.sb[SB_TI + b * NX * NX + i * NX + j], rv[j], yv);
+            for (int j = 0; j < NX; ++j) yv = fma(ti[b][j], rv[j], yv);
             yvs[b] = yv;
             if (b >= 1) {
-                const double* V = L.sb + SB_V + b * 256;
                 double yu[NX];
 #pragma unroll
                 for (int j = 0; j < NX; ++j) yu[j] = readlane_d(yv, j);
-                double p1 = L.P[(size_t)seg_start(b, H) * PPB + PO + i];
+                double p1 = p1s[b];
 #pragma unroll
-                for (int l = 0; l < NX; ++l) p1 = fma(V[i * 16 + LI + l], yu[l], p1);
+                for (int l = 0; l < NX; ++l) p1 = fma(vxl[b][l], yu[l], p1);
                 phv = p1;
             }
         }
@@ -1996,25 +2038,36 @@ struct SqpKernel {
         for (int e = k0 * NX + lane; e < k1 * NX; e += 64) {
             const int k = e / NX, i = e - k * NX;
             const double* Kk = L.K + (size_t)k * NU * KST;
+            const double* G = L.G + (size_t)k * NX * GS + i * GS;
+            double* Pk = L.P + (size_t)k * PPB;
+            double* kp = i < NU ? L.K + (size_t)k * NU * KST + min(i, NU - 1) * KST + NX : L.dummy + lane;
+            // every load first (before a scheduling barrier), stores branch-free (dummy slots for the
+            // other lanes)
+            double kl[NU][NX], gb[NU], pxl[NX];
+#pragma unroll
+            for (int a = 0; a < NU; ++a) {
+                gb[a] = G[NX + a];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) kl[a][j] = Kk[a * KST + NX + 1 + j];
+            }
+#pragma unroll
+            for (int j = 0; j < NX; ++j) pxl[j] = Pk[PXL + i * NX + j];
+            double ac = L.Acl[(size_t)k * NX * PS + i * PS + NX];
+            double pv = Pk[PO + i];
+            const double kv = *kp;
+            __builtin_amdgcn_sched_barrier(0);
             double dk[NU];   // K_lambda,k lambda
 #pragma unroll
             for (int a = 0; a < NU; ++a) {
                 double acc = 0.0;
 #pragma unroll
-                for (int j = 0; j < NX; ++j) acc = fma(Kk[a * KST + NX + 1 + j], lam[j], acc);
+                for (int j = 0; j < NX; ++j) acc = fma(kl[a][j], lam[j], acc);
                 dk[a] = acc;
             }
-            const double* G = L.G + (size_t)k * NX * GS + i * GS;
-            double ac = L.Acl[(size_t)k * NX * PS + i * PS + NX];
 #pragma unroll
-            for (int a = 0; a < NU; ++a) ac = fma(G[NX + a], dk[a], ac);
-            double* Pk = L.P + (size_t)k * PPB;
-            double pv = Pk[PO + i];
+            for (int a = 0; a < NU; ++a) ac = fma(gb[a], dk[a], ac);
 #pragma unroll
-            for (int j = 0; j < NX; ++j) pv = fma(Pk[PXL + i * NX + j], lam[j], pv);
-            // every load before the first store, stores branch-free (dummy slots for the other lanes)
-            double* kp = i < NU ? L.K + (size_t)k * NU * KST + min(i, NU - 1) * KST + NX : L.dummy + lane;
-            const double kv = *kp;
+            for (int j = 0; j < NX; ++j) pv = fma(pxl[j], lam[j], pv);
             L.Acl[(size_t)k * NX * PS + i * PS + NX] = ac;
             *(k >= 1 ? Pk + PO + i : L.dummy + lane) = pv;
             *kp = kv + dk[i < NU ? i : 0];
