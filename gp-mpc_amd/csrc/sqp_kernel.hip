@@ -1282,39 +1282,71 @@ struct SqpKernel {
         double* VT = L.dxv;
         // entries (k, i) two per pass, both computed before either is stored (T and VT alias other
         // LDS buffers, so a store would otherwise order the next entry's reads behind it)
+        // (each pass issues every load of its entries before a scheduling barrier: loads interleaved
+        // with their uses issue a few at a time)
         const int n = H * NX;
-        auto t_entry = [&](int e) {
+        struct TOps { double pr[NX], gc[NX]; };
+        auto t_load = [&](int e, TOps& o) {
             const int k = e / NX, i = e - k * NX;
             const double* Pn = L.P + (size_t)(k + 1) * PP;
             const double* G = L.G + (size_t)k * NX * GS;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                o.pr[l] = Pn[i <= l ? pidx(i, l) : pidx(l, i)];
+                o.gc[l] = G[l * GS + NB];
+            }
+        };
+        auto t_dot = [](const TOps& o) {
             double acc = 0.0;
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
+            for (int l = 0; l < NX; ++l) acc = fma(o.pr[l], o.gc[l], acc);
             return acc;
         };
         for (int e0 = lane; e0 < n; e0 += 128) {
             const int e1 = e0 + 64;
             const bool has1 = e1 < n;
-            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            TOps o0, o1;
+            t_load(e0, o0);
+            t_load(has1 ? e1 : e0, o1);
+            __builtin_amdgcn_sched_barrier(0);
+            const double a0 = t_dot(o0), a1 = t_dot(o1);
             T[e0] = a0;
             if (has1) T[e1] = a1;
         }
         WSYNC();
-        auto vt_entry = [&](int e) {
+        struct VOps { double g0, gu[NU], kc[NU], ac[NX], tk[NX]; };
+        auto vt_load = [&](int e, VOps& o) {
             const int k = e / NX, i = e - k * NX;
             const double* A = L.Acl + (size_t)k * NX * PS;
             const double* Kk = L.K + (size_t)k * NU * PS;
-            double acc = L.gq[k * NBS + i];
+            o.g0 = L.gq[k * NBS + i];
 #pragma unroll
-            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * PS + i], L.gq[k * NBS + NX + a], acc);
+            for (int a = 0; a < NU; ++a) {
+                o.kc[a] = Kk[a * PS + i];
+                o.gu[a] = L.gq[k * NBS + NX + a];
+            }
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
+            for (int l = 0; l < NX; ++l) {
+                o.ac[l] = A[l * PS + i];
+                o.tk[l] = T[k * NX + l];
+            }
+        };
+        auto vt_dot = [](const VOps& o) {
+            double acc = o.g0;
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc = fma(o.kc[a], o.gu[a], acc);
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(o.ac[l], o.tk[l], acc);
             return acc;
         };
         for (int e0 = lane; e0 < n; e0 += 128) {
             const int e1 = e0 + 64;
             const bool has1 = e1 < n;
-            const double a0 = vt_entry(e0), a1 = vt_entry(has1 ? e1 : e0);
+            VOps o0, o1;
+            vt_load(e0, o0);
+            vt_load(has1 ? e1 : e0, o1);
+            __builtin_amdgcn_sched_barrier(0);
+            const double a0 = vt_dot(o0), a1 = vt_dot(o1);
             VT[e0] = a0;
             if (has1) VT[e1] = a1;
         }
@@ -1351,13 +1383,24 @@ struct SqpKernel {
             const int k = e / NU, a = e - k * NU;
             const double* G = L.G + (size_t)k * NX * GS;
             const double* pn = L.P + (size_t)(k + 1) * PP + PO;
+            double gb[NU][NX], tp[NX], gqv[NU], rui[NU];
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                gqv[b2] = L.gq[k * NBS + NX + b2];
+                rui[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) gb[b2][l] = G[l * GS + NX + b2];
+            }
+#pragma unroll
+            for (int l = 0; l < NX; ++l) tp[l] = T[k * NX + l] + pn[l];
+            __builtin_amdgcn_sched_barrier(0);
             double kf = 0.0;
 #pragma unroll
             for (int b2 = 0; b2 < NU; ++b2) {
-                double acc = L.gq[k * NBS + NX + b2];
+                double acc = gqv[b2];
 #pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + NX + b2], T[k * NX + l] + pn[l], acc);
-                kf = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], acc, kf);
+                for (int l = 0; l < NX; ++l) acc = fma(gb[b2][l], tp[l], acc);
+                kf = fma(rui[b2], acc, kf);
             }
             L.K[(size_t)k * NU * PS + a * PS + NX] = -kf;
         }
@@ -1683,38 +1726,69 @@ struct SqpKernel {
         double* T = L.hq;
         double* VT = L.dxv;
         const int n = k1 * NX;
-        auto t_entry = [&](int e) {
+        // (each pass issues every load of its entries before a scheduling barrier)
+        struct TOps { double pr[NX], gc[NX]; };
+        auto t_load = [&](int e, TOps& o) {
             const int k = e / NX, i = e - k * NX;
             const double* Pn = L.P + (size_t)(k + 1) * PPB;
             const double* G = L.G + (size_t)k * NX * GS;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                o.pr[l] = Pn[i <= l ? pidx(i, l) : pidx(l, i)];
+                o.gc[l] = G[l * GS + NB];
+            }
+        };
+        auto t_dot = [&](int e, const TOps& o) {
             double acc = 0.0;
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(Pn[i <= l ? pidx(i, l) : pidx(l, i)], G[l * GS + NB], acc);
-            return (last || k + 1 < k1) ? acc : 0.0;
+            for (int l = 0; l < NX; ++l) acc = fma(o.pr[l], o.gc[l], acc);
+            return (last || e / NX + 1 < k1) ? acc : 0.0;
         };
         for (int e0 = k0 * NX + lane; e0 < n; e0 += 128) {
             const int e1 = e0 + 64;
             const bool has1 = e1 < n;
-            const double a0 = t_entry(e0), a1 = t_entry(has1 ? e1 : e0);
+            TOps o0, o1;
+            t_load(e0, o0);
+            t_load(has1 ? e1 : e0, o1);
+            __builtin_amdgcn_sched_barrier(0);
+            const double a0 = t_dot(e0, o0), a1 = t_dot(has1 ? e1 : e0, o1);
             T[e0] = a0;
             if (has1) T[e1] = a1;
         }
         WSYNC();
-        auto vt_entry = [&](int e) {
+        struct VOps { double g0, gu[NU], kc[NU], ac[NX], tk[NX]; };
+        auto vt_load = [&](int e, VOps& o) {
             const int k = e / NX, i = e - k * NX;
             const double* A = L.Acl + (size_t)k * NX * PS;
             const double* Kk = L.K + (size_t)k * NU * KST;
-            double acc = L.gq[k * NBS + i];
+            o.g0 = L.gq[k * NBS + i];
 #pragma unroll
-            for (int a = 0; a < NU; ++a) acc = fma(Kk[a * KST + i], L.gq[k * NBS + NX + a], acc);
+            for (int a = 0; a < NU; ++a) {
+                o.kc[a] = Kk[a * KST + i];
+                o.gu[a] = L.gq[k * NBS + NX + a];
+            }
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc = fma(A[l * PS + i], T[k * NX + l], acc);
+            for (int l = 0; l < NX; ++l) {
+                o.ac[l] = A[l * PS + i];
+                o.tk[l] = T[k * NX + l];
+            }
+        };
+        auto vt_dot = [](const VOps& o) {
+            double acc = o.g0;
+#pragma unroll
+            for (int a = 0; a < NU; ++a) acc = fma(o.kc[a], o.gu[a], acc);
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc = fma(o.ac[l], o.tk[l], acc);
             return acc;
         };
         for (int e0 = k0 * NX + lane; e0 < n; e0 += 128) {
             const int e1 = e0 + 64;
             const bool has1 = e1 < n;
-            const double a0 = vt_entry(e0), a1 = vt_entry(has1 ? e1 : e0);
+            VOps o0, o1;
+            vt_load(e0, o0);
+            vt_load(has1 ? e1 : e0, o1);
+            __builtin_amdgcn_sched_barrier(0);
+            const double a0 = vt_dot(o0), a1 = vt_dot(o1);
             VT[e0] = a0;
             if (has1) VT[e1] = a1;
         }
@@ -1748,15 +1822,30 @@ struct SqpKernel {
         for (int e = k0 * NU + lane; e < k1 * NU; e += 64) {
             const int k = e / NU, a = e - k * NU;
             const double* G = L.G + (size_t)k * NX * GS;
-            const bool pz = !last && k + 1 == k1;   // segment end: p_k1 = 0
+            const unsigned mz = (!last && k + 1 == k1) ? 0xffffffffu : 0u;   // segment end: p_k1 = 0
             const double* pn = L.P + (size_t)(k + 1) * PPB + PO;
+            // every load first (before a scheduling barrier), the p_k1 = 0 select branch-free
+            double gb[NU][NX], tk[NX], pv[NX], gqv[NU], rui[NU];
+#pragma unroll
+            for (int b2 = 0; b2 < NU; ++b2) {
+                gqv[b2] = L.gq[k * NBS + NX + b2];
+                rui[b2] = L.Rui[(size_t)k * NU * NU + a * NU + b2];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) gb[b2][l] = G[l * GS + NX + b2];
+            }
+#pragma unroll
+            for (int l = 0; l < NX; ++l) {
+                tk[l] = T[k * NX + l];
+                pv[l] = pn[l];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             double kf = 0.0;
 #pragma unroll
             for (int b2 = 0; b2 < NU; ++b2) {
-                double acc = L.gq[k * NBS + NX + b2];
+                double acc = gqv[b2];
 #pragma unroll
-                for (int l = 0; l < NX; ++l) acc = fma(G[l * GS + NX + b2], T[k * NX + l] + (pz ? 0.0 : pn[l]), acc);
-                kf = fma(L.Rui[(size_t)k * NU * NU + a * NU + b2], acc, kf);
+                for (int l = 0; l < NX; ++l) acc = fma(gb[b2][l], tk[l] + bsel(mz, 0.0, pv[l]), acc);
+                kf = fma(rui[b2], acc, kf);
             }
             L.K[(size_t)k * NU * KST + a * KST + NX] = -kf;
         }
