@@ -493,9 +493,14 @@ struct SqpKernel {
                 gp_tiles_dispatch<NWAVES>(g.tX, g.tW, g.ntile, zb, cz, so, lane, ne, 0);
                 __syncthreads();   // B2: partial sums of every wave written
                 for (int e = lane; e < np * 4; e += 64) {
-                    double v = so[e];
+                    double part[NWAVES];   // every load before the sum (scheduling barrier)
+                    part[0] = so[e];
 #pragma unroll
-                    for (int w = 1; w < NWAVES; ++w) v += L.gsh[(size_t)(w - 1) * np * 4 + e];
+                    for (int w = 1; w < NWAVES; ++w) part[w] = L.gsh[(size_t)(w - 1) * np * 4 + e];
+                    __builtin_amdgcn_sched_barrier(0);
+                    double v = part[0];
+#pragma unroll
+                    for (int w = 1; w < NWAVES; ++w) v += part[w];
                     so[e] = v;
                 }
             }
