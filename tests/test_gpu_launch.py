@@ -159,3 +159,47 @@ def test_cost_ordered_dispatch_is_bit_exact():
         assert (outs[-1][1] == 0).float().mean() > 0.9
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("waves", [2, 4])
+@pytest.mark.parametrize("name,N,H", [("quad2d", 60, 4), ("quad2d", 60, 5), ("quad2d", 60, 7), ("quad2d", 60, 45),
+                                      ("cartpole", 40, 4), ("cartpole", 40, 11), ("cartpole", 40, 40)])
+def test_segment_solve_matches_one_segment_recursion(name, N, H, waves):
+    """The segment-parallel Newton solve (two segments on two waves, three on four) against the
+    same launch shape with one wave running the whole recursion, on the same closed loop at KKT
+    1e-9: identical status, x and u within 1e-6 (1 + |.|).  Horizons down to H = 4 (segments of
+    one stage), uneven splits (5, 7, 11) and past the split-lane IPM layout (H = 40, 45)."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    spec, data, hyp = problem(name, N)
+    mats = lqr(spec)
+    B, steps = 8, 3
+    solvers = []
+    for seg in (0, 1):
+        gs = BatchSolver(spec, H, B, tol=1e-9, qp_tol=1e-11, qp_max_iter=100)
+        gs.set_launch(waves=waves)
+        gs.set_tuning(seg=seg)
+        gs.set_gps(product_gps(data, hyp))
+        gs.set_tightening(True, 0.95, *mats)
+        gs.reset(reset_iterate=True)
+        assert gs.launch_info()["segments"] == (1 if seg == 0 else (3 if waves == 4 else 2))
+        solvers.append(gs)
+    traj = spec.reference_trajectory()
+    x0, phase = initial_states(spec, traj, B)
+    x = torch.tensor(x0, device="cuda")
+    for s in range(steps):
+        ph = torch.tensor(phase + s, dtype=torch.int32, device="cuda")
+        outs = []
+        for gs in solvers:
+            u = gs.solve(x, ph).clone()
+            xs, us, _ = (t.cpu().numpy() for t in gs.solution())
+            outs.append((gs.status.cpu().numpy(), xs, us, u))
+        (st0, x_0, u_0, c0), (st1, x_1, u_1, _) = outs
+        np.testing.assert_array_equal(st0, st1)
+        ok = st0 == 0
+        assert ok.sum() >= B - 1, (s, st0)
+        ex = np.abs(x_1 - x_0).max(axis=(1, 2)) / (1 + np.abs(x_0).max(axis=(1, 2)))
+        eu = np.abs(u_1 - u_0).max(axis=(1, 2)) / (1 + np.abs(u_0).max(axis=(1, 2)))
+        assert max(ex[ok].max(), eu[ok].max()) <= 1e-6, (s, ex[ok].max(), eu[ok].max())
+        x = solvers[0].plant_step(x, c0)
