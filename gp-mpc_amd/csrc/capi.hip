@@ -269,7 +269,7 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.lin_gen = 1;   // tags start at 0: nothing cached
     P.waves = 0;            // automatic launch shape (gpmpc_set_launch)
     P.order_dispatch = 1;   // cost-ordered dispatch of multi-round launches (GPMPC_TUNE_ORDER)
-    P.seg = 1;              // two-segment Newton solves (GPMPC_TUNE_SEG)
+    P.seg = 1;              // segment-parallel Newton solves (GPMPC_TUNE_SEG)
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;

@@ -85,7 +85,7 @@ struct ProblemDev {
     // cost-ordered dispatch (StateDev::order): on when a launch has more instances than the
     // device holds at once (gpmpc_set_tuning GPMPC_TUNE_ORDER: 0 off, 2 ranks every launch)
     int32_t order_dispatch;
-    // two-segment Newton solves when the launch runs two or four waves per instance (single-tile
+    // segment-parallel Newton solves when the launch runs two or four waves per instance (single-tile
     // models; gpmpc_set_tuning GPMPC_TUNE_SEG)
     int32_t seg;
     GPDev gp[kMaxGP];

@@ -328,7 +328,7 @@ struct SqpKernel {
     // true P'_H.  lambda takes tile slots LI .. LI + NX - 1; a P' block then also carries P_x,lambda
     // (NX x NX at PXL) and K'_k = [K | kff | K_lambda] (row stride KST).
     static constexpr bool kSeg = SEG;
-    static_assert(!SEG || (NW >= 2 && NB + 1 <= 16 && NX + 1 <= 8), "two-segment solve: single-tile models on >= 2 waves");
+    static_assert(!SEG || (NW >= 2 && NB + 1 <= 16 && NX + 1 <= 8), "segment-parallel solve: single-tile models on >= 2 waves");
     static constexpr int LI = 8 + NU;
     static_assert(!SEG || LI + NX <= 16, "lambda slots in the 16-wide tile");
     static constexpr int KST = SEG ? 2 * NX + 1 : PS;          // K' row stride
@@ -1449,7 +1449,8 @@ struct SqpKernel {
 
     // ------------------------------------------------------------------ segment-parallel Newton solve (kSeg)
     // Segment w = stages seg_start(w) .. seg_start(w + 1) - 1 on wave seg_wave(w) (tools/seg2_proto.py
-    // is the numpy model of the two-segment form against the dense KKT solve).
+    // is the numpy model of the two-segment form, tests/test_segment_model_cpu.py of any count, against
+    // the dense KKT solve).
     __host__ __device__ static int seg_start(int w, int H) { return (w * H) / NSEG; }
     __device__ static int lam_of(int t) { return (t >= LI && t < LI + NX) ? t - LI : -1; }
 
@@ -2168,7 +2169,7 @@ struct SqpKernel {
         }
     }
 
-    // Per-lane step from the two-segment solution: recover_step_mfma with the KST / PPB strides (the
+    // Per-lane step from the segment-parallel solution: recover_step_mfma with the KST / PPB strides (the
     // boundary costate is already folded into segment A's kff and p, seg_fold).
     __device__ static void recover_step_seg(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
         const bool on = lane <= H;
@@ -3416,7 +3417,7 @@ int sqp_waves(const ProblemDev& P, int batch) {
     }
 }
 
-// two-segment Newton solves (SqpKernel::kSeg): the single-tile models on two or four waves per
+// segment-parallel Newton solves (SqpKernel::kSeg): the single-tile models on two or four waves per
 // instance, when the option allows it (P.seg) and each segment has at least two stages
 static bool sqp_seg_of(const ProblemDev& P, int nw) { return P.seg != 0 && nw >= 2 && P.H >= 4; }
 

@@ -73,7 +73,8 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
 @pytest.mark.parametrize("name,N,H,B,steps", [("quad2d", 200, 30, 12, 4), ("cartpole", 50, 20, 12, 4),
                                                ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
 def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, seg):
-    """seg = 1: the two-segment Newton solve (gpmpc_set_tuning GPMPC_TUNE_SEG) on two or four waves."""
+    """seg = 1: the segment-parallel Newton solve (gpmpc_set_tuning GPMPC_TUNE_SEG): two segments on
+    two waves, three on four."""
     # quad2d N=200 H=30: one of the 12 instances needs more than 25 SQP iterations for KKT 1e-9 at
     # step 1 (Gauss-Newton's linear rate; the C++ restatement stops there too)
     _run_against_cpp(name, N, H, B, steps, waves, all_converge=not (name == "quad2d" and H == 30), seg=seg)
