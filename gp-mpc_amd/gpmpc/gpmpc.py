@@ -93,6 +93,15 @@ class GPMPC:
         self._u_prev = None
         self._has_prev = False
         self._tstep = torch.zeros(self.batch, dtype=torch.int32, device=self.device)
+        # select_action's host staging: pinned buffers, so the observation / reference index go in and
+        # the action / status come back as asynchronous copies with one synchronisation per call
+        self._pinned = None
+        if self.batch == 1 and torch.device(self.device).type == "cuda":
+            self._pinned = (torch.empty(1, spec.nx, dtype=torch.float64, pin_memory=True),
+                            torch.empty(1, dtype=torch.int32, pin_memory=True),
+                            torch.empty(spec.nu, dtype=torch.float64, pin_memory=True),
+                            torch.empty(1, dtype=torch.int32, pin_memory=True))
+            self._x0_dev = torch.empty(1, spec.nx, dtype=torch.float64, device=self.device)
 
     @staticmethod
     def _gp_columns(spec: ModelSpec) -> list[list[int]]:
@@ -244,15 +253,30 @@ class GPMPC:
         assert not self._requires_recompile, "GP model must be uploaded (call reset())"
         assert self.gaussian_process is not None, "Gaussian processes are not initialized"
         assert self.batch == 1, "select_action is the single-instance form; use select_action_batch"
-        x0 = torch.as_tensor(np.asarray(obs, dtype=np.float64).reshape(1, -1), device=self.device)
-        self._tstep.fill_(self.traj_step)
-        self.traj_step += 1
-        u0 = self.solver.solve(x0, self._tstep)
-        status = int(self.solver.status[0].item())
+        if self._pinned is None:
+            x0 = torch.as_tensor(np.asarray(obs, dtype=np.float64).reshape(1, -1), device=self.device)
+            self._tstep.fill_(self.traj_step)
+            self.traj_step += 1
+            u0 = self.solver.solve(x0, self._tstep)
+            status = int(self.solver.status[0].item())
+            u = u0[0].cpu().numpy()
+        else:
+            x_h, t_h, u_h, s_h = self._pinned
+            x_h.numpy()[0] = np.asarray(obs, dtype=np.float64).reshape(-1)
+            t_h[0] = self.traj_step
+            self.traj_step += 1
+            self._x0_dev.copy_(x_h, non_blocking=True)
+            self._tstep.copy_(t_h, non_blocking=True)
+            u0 = self.solver.solve(self._x0_dev, self._tstep)
+            u_h.copy_(u0[0], non_blocking=True)
+            s_h.copy_(self.solver.status[:1], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            status = int(s_h[0])
+            u = u_h.numpy().copy()
         assert status in [0, 2], f"solver returned unexpected status {status} ({STATUS_NAMES.get(status)})."
         self._has_prev = True
         self._x_prev = self._u_prev = None
-        return u0[0].cpu().numpy()
+        return u
 
     def select_action_batch(self, obs: torch.Tensor, tstep: torch.Tensor | None = None, check: bool = False):
         """Batched select_action on device tensors: obs (B, nx) float64 -> actions (B, nu).
