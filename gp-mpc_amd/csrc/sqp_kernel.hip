@@ -2246,8 +2246,15 @@ struct SqpKernel {
                 if (lane == 0) L.ctrl[8 + sg] = fok ? 1 : 0;
             }
             __syncthreads();   // Bm1
+            {   // every segment's status flag loaded at once (a short-circuit && loads them one by one)
+                int f[NSEG];
 #pragma unroll
-            for (int q = 0; q < NSEG; ++q) ok = ok && L.ctrl[8 + q] != 0;
+                for (int q = 0; q < NSEG; ++q) f[q] = L.ctrl[8 + q];
+                int all = 1;
+#pragma unroll
+                for (int q = 0; q < NSEG; ++q) all &= (f[q] != 0) ? 1 : 0;
+                ok = all != 0;
+            }
             if (chain && ok) seg_chain_full(L, H, lane);
             if (a1 > a0) seg_acl<true>(L, lane, a0, a1);
             __syncthreads();   // Bm2: lambda_b, x_w, A'_k
