@@ -201,6 +201,13 @@ def single_instance_gpu(spec, gps, H, lqr_mats, x0, phase, warmup, steps, dev, q
                       f"timed with perf_counter after {warmup} untimed; host_ms = wall - kernel events"}
 
 
+def _build_info():
+    """Provenance of the library this run loaded (gpmpc_build_id against the tree's source hash)."""
+    from gpmpc import _lib
+
+    return _lib.build_info()
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -438,10 +445,15 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         tot = stats_buf.sum(0).to(torch.float64)
         mx = stats_buf.max(0).values.to(torch.float64)
         sums, status_counts, maxes = torch.cat([tot[:2], tot[9:10]]), tot[2:7].clone(), mx[7:9].clone()
+        # per-instance solve time inside the SQP kernel (s_memrealtime, 100 MHz ticks, slot 10 summed over
+        # the timed steps): the slowest instance's and the mean, for the roofline's latency block
+        inst = torch.stack([mx[10], tot[10]])
         if dist is not None:
             dist.all_reduce(sums, op=dist.ReduceOp.SUM)
             dist.all_reduce(status_counts, op=dist.ReduceOp.SUM)
             dist.all_reduce(maxes, op=dist.ReduceOp.MAX)
+            dist.all_reduce(inst[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(inst[1:], op=dist.ReduceOp.SUM)
         # instance-steps the statistics cover: every rank's (all-reduced) or, for an emulated shard
         # (no process group), this shard's own
         n_is = (B if emulated else total_instances) * args.steps
@@ -449,7 +461,9 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
                 "var_list": var_list, "sqp_sum": sqp_sum, "var_sum": var_sum, "x0_all": x0_all,
                 "phase_all": phase_all, "value": total_instances * args.steps / elapsed,
                 "sqp_mean": float(sums[0]) / n_is, "lin_mean": float(sums[2]) / n_is, "qp_mean": float(sums[1]) / n_is,
-                "status_counts": status_counts, "maxes": maxes}
+                "status_counts": status_counts, "maxes": maxes,
+                "inst_ms_max": float(inst[0]) * 1e-5 / args.steps,                       # slowest instance
+                "inst_ms_mean": float(inst[1]) * 1e-5 / args.steps / (B if emulated else total_instances)}
 
     # instances of this rank: contiguous global ids (strong: the rank's slice of the global batch;
     # weak: rank*B .. rank*B+B-1), no collective in the data path
@@ -484,8 +498,14 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
         # overlapped: the SQP flops over the step's whole kernel span (variance + SQP spans), a lower
         # bound on the SQP kernel's rate; the kernel's own duration comes from a rocprofv3 trace
         sqp_basis_ms = sqp_ms + (var_ms if var_list else 0.0) if overlapped else sqp_ms
-        flops_sqp = B * lin_mean * per_lin          # per launch (one rank's batch)
-        achieved = flops_sqp / (sqp_basis_ms * 1e-3) / 1e12
+        # SURVEY.md §8(d)'s count: F_mean = K_sqp H 4 sum_g N_g (4 d_g + 2) per instance-step with
+        # K_sqp = sqp_iter_mean (every GP at the 4 RK4 points of every SQP iteration), per launch
+        flops_8d = B * sqp_mean * survey_flops_per_lin(spec, N, H)
+        achieved = flops_8d / (sqp_basis_ms * 1e-3) / 1e12
+        # what the kernel executes: linearisations computed (slot 9: one per SQP iteration plus the
+        # converged iterate's, minus the cached one), u-only GPs once per stage
+        flops_exec = B * lin_mean * per_lin
+        achieved_exec = flops_exec / (sqp_basis_ms * 1e-3) / 1e12
         var_tf = (B * var_flops) / (var_ms * 1e-3) / 1e12 if var_list and not overlapped else None
         exps_launch = B * lin_mean * exps_lin
         workload = workload_name(spec, args, world)
@@ -529,20 +549,31 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
                        "model": spec.name, "global_batch": total_instances, "horizon": H, "n_train": N,
                        "batch_per_gpu": B,
                        "parallelism": f"instances sharded over {world} GPU(s) in contiguous slices, GP replicated"},
-            "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "achieved": achieved,
-                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "note": "FP64 GP mean+gradient contraction flops executed (linearisations computed, "
-                                 "u-only GPs once per stage) / HIP-event kernel time; peak = FP64 dense (vector = "
-                                 "matrix on gfx950); the kernel is latency-bound in the Riccati recursion",
+            "roofline": {"kernel": "sqp_step_kernel", "bound": "mfma", "regime": "latency",
+                         "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_src,
+                         "flops_per_launch": flops_8d,
+                         "count": "SURVEY.md 8(d): F_mean = K_sqp * H * 4 * sum_g N_g (2 d_g + 2 (d_g + 1)) per "
+                                  "instance-step, K_sqp = sqp_iter_mean; x instances of the launch",
+                         "note": "the FP64 MFMA peak is the ceiling the fraction is priced against (the GP sums are "
+                                 "the kernel's one dense contraction); the kernel does not run at that ceiling: it "
+                                 "is latency-bound, set by its slowest instance's sequential recursions (latency)",
                          "time_basis": ("overlapped step: SQP flops over the step's whole kernel span (variance + "
                                         "SQP event spans, a lower bound on the SQP kernel's rate)") if overlapped
                                        else "SQP-kernel HIP events",
-                         "achieved_survey_8d": B * (sqp_mean + 1.0) * survey_flops_per_lin(spec, N, H)
-                                               / (sqp_basis_ms * 1e-3) / 1e12,
-                         "note_survey_8d": "SURVEY.md 8(d)'s algorithmic count: (sqp_iter + 1) linearisations "
-                                           "per step, every GP at the 4 RK4 points, as the reference computes "
-                                           "them; informational, not the frac above"},
+                         "latency": {"slowest_instance_ms_per_step": m["inst_ms_max"],
+                                     "mean_instance_ms_per_step": m["inst_ms_mean"],
+                                     "kernel_ms_per_step": sqp_basis_ms,
+                                     "slowest_over_kernel": m["inst_ms_max"] / sqp_basis_ms,
+                                     "slowest_over_mean": m["inst_ms_max"] / max(m["inst_ms_mean"], 1e-12),
+                                     "note": "each instance's time inside the SQP kernel (s_memrealtime, first to last "
+                                             "instruction of its workgroup, stats slot 10) summed over the timed steps; "
+                                             "slowest_over_kernel near 1: the launch lasts as long as its slowest "
+                                             "instance's critical path"},
+                         "executed": {"achieved": achieved_exec, "frac": achieved_exec / FP64_PEAK_TFLOPS,
+                                      "flops_per_launch": flops_exec,
+                                      "note": "flops the kernel executes: linearisations computed (the cached one "
+                                              "skipped, the converged iterate's included), u-only GPs once per stage"}},
             "roofline_variance": None if var_tf is None else {
                 "kernel": ((f"gp_love_kernel<true> (LOVE root ranks {'/'.join(str(r) for r in solver.love_ranks if r)}, "
                             f"full tiles/quads {'/'.join('%d+%d' % love_tiles(r) for r in solver.love_ranks if r)})")
@@ -579,6 +610,7 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
             "weak_per_gpu": weak,
             "single_instance_gpu": single,
             "cpu_baseline": cpu,
+            "build": _build_info(),
         }
         if emulated:
             out["emulated_shard"] = {"rank": rank, "world": world, "instances": [ids.start, ids.stop],

@@ -12,7 +12,7 @@ constexpr int kMaxNU = 4;
 constexpr int kMaxH = 63;       // one lane per stage 0..H (64-lane wavefront)
 constexpr int kPhases = 12;  // diagnostic phase slots (GPMPC_TIMING builds)
 constexpr int kMaxParams = 16;
-constexpr int kStatsSlots = 10;  // per-instance solver statistics (gpmpc_set_stats_buffer, = GPMPC_STATS_SLOTS)
+constexpr int kStatsSlots = 12;  // per-instance solver statistics (gpmpc_set_stats_buffer, = GPMPC_STATS_SLOTS)
 
 enum ModelId : int32_t { kQuad2D = 0, kQuad3D = 1, kCartpole = 2 };
 
@@ -132,7 +132,8 @@ struct StepIO {
     unsigned long long* timing;  // [B][kPhases] phase cycles (GPMPC_TIMING builds only), may be null
     long long* stats;            // [B][kStatsSlots] sqp iters, qp iters (sums), status 0..4 counts,
                                  // max sqp iters, max qp iters per solve, linearisations
-                                 // computed; may be null
+                                 // computed, the instance's solve time in s_memrealtime ticks
+                                 // (sum; the last solve's); may be null
 };
 
 // Arguments of the GP posterior kernel (gp_kernels.hip).

@@ -1913,11 +1913,18 @@ struct SqpKernel {
     // column read by v_readlane), and [Y_b | y_b | T_b^-1] = Ph x (the eliminated right-hand sides).
     // Then seg_chain_forward.  T_b^-1, Y_b and the computed cost-to-go matrices stay in the boundary
     // data for the corrector.
-    __device__ static void seg_chain_full(const Lds& L, int H, int lane) {
+    // M is positive definite only while Ph is: a state direction that no cost, bound barrier or
+    // coupling reaches (q_i = 0 on an unbounded or barely bounded state) leaves Ph singular and a
+    // pivot at rounding level.  Every pivot is checked against the largest diagonal entry of M
+    // (kPivRel): the return value false sends the solve to the one-segment recursion (seg_part's
+    // fallback), which never inverts Ph.
+    static constexpr double kPivRel = 1e-12;
+    __device__ static bool seg_chain_full(const Lds& L, int H, int lane) {
         constexpr int CI = NX;
         const int c = min(lane, 3 * NX);
         const int cm = min(c, NX - 1);
         const unsigned mcol = c < NX ? 0xffffffffu : 0u;
+        bool piv_ok = true;
         for (int b = NSEG - 2; b >= 0; --b) {
             const double* V = L.sb + SB_V + b * 256;
             const double* Pm = (b == NSEG - 2) ? L.P + (size_t)seg_start(NSEG - 1, H) * PPB : L.sb + SB_PH + b * PP;
@@ -1954,11 +1961,15 @@ struct SqpKernel {
                 for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], bv[l], acc);
                 col[i] = acc;
             }
+            double dmx = 0.0;   // largest diagonal entry of M (lane i holds column i)
+#pragma unroll
+            for (int i = 0; i < NX; ++i) dmx = fmax(dmx, readlane_d(col[i], i));
 #pragma unroll
             for (int p = 0; p < NX; ++p) {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
+                piv_ok = piv_ok && (cp[p] > kPivRel * dmx);   // (false for a NaN pivot too)
                 const double inv = fast_rcp(cp[p]);
                 col[p] *= inv;
 #pragma unroll
@@ -2010,6 +2021,7 @@ struct SqpKernel {
         }
         WSYNC();   // y_b, Y_b of every boundary before the forward pass reads them on other lanes
         seg_chain_forward(L, lane, false);
+        return piv_ok;
     }
 
     // Forward over the boundaries from x_0 = 0: lambda_b = Y_b x_b + y_b (boundary 0: y_0),
@@ -2214,8 +2226,14 @@ struct SqpKernel {
     //                 Bm2 | forward sweeps (after the fold of each segment's lambda) | B2
     //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain, others: affine columns |
     //                 Bm2 | forward | B2
-    // Factorisation statuses in ctrl[8 + w].
+    // Factorisation statuses in ctrl[8 + w].  Fallback: when the boundary chain meets a pivot it cannot
+    // trust (seg_chain_full), it sets ctrl[kFb]; after Bm2 the chain wave then runs the one-segment
+    // recursion over the whole horizon in the same layout (factorisation into ctrl[kFb + 1], closed-loop
+    // maps, forward sweep from dx_0 = 0) before B2, and the corrector of the same IPM iteration runs its
+    // one-segment vector pass, maps and sweep between B1 and Bm1.  Same barriers on every wave.
     static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
+    static constexpr int kFb = 12;   // ctrl slots: fallback flag, fallback factorisation status
+    static constexpr int kTs = 14;   // ctrl slots 14-15: the instance's start time stamp (stats slot 10)
     __host__ __device__ static constexpr int seg_of_wave(int w) { return NSEG == 3 ? w - 1 : (w == 1 ? 0 : (w == 0 ? 1 : -1)); }
     // KIND 0: no segment on this wave; 1: segment sg < NSEG - 1 (lambda recursion); 2: the last segment
     // The closed-loop maps A'_k (seg_acl) are formed between Bm1 and Bm2, while wave 1 runs the boundary
@@ -2255,10 +2273,14 @@ struct SqpKernel {
                 for (int q = 0; q < NSEG; ++q) all &= (f[q] != 0) ? 1 : 0;
                 ok = all != 0;
             }
-            if (chain && ok) seg_chain_full(L, H, lane);
+            if (chain && ok) {
+                const bool cok = seg_chain_full(L, H, lane);
+                if (lane == 0) L.ctrl[kFb] = cok ? 0 : 1;
+            }
             if (a1 > a0) seg_acl<true>(L, lane, a0, a1);
             __syncthreads();   // Bm2: lambda_b, x_w, A'_k
-            if (ok) {
+            const bool fb = ok && L.ctrl[kFb] != 0;
+            if (ok && !fb) {
                 if constexpr (KIND == 1) {
                     seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
                     WSYNC();
@@ -2267,20 +2289,41 @@ struct SqpKernel {
                     seg_forward(L, lane, k0, H, xs, true);
                 }
             }
-            __syncthreads();   // B2
-        } else {
-            if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
-            if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
-            __syncthreads();   // Bm1
-            if (chain) seg_chain_vec(L, H, lane);
-            if (a1 > a0) seg_acl<false>(L, lane, a0, a1);
-            __syncthreads();   // Bm2: lambda_b, x_w, A'_k[:, CI]
-            if constexpr (KIND == 1) {
-                seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
+            if (fb && chain) {   // the one-segment recursion instead (Ph singular at a boundary)
+                const bool fok = seg_factor<false>(L, H, lane, 0, H, nullptr);
+                if (lane == 0) L.ctrl[kFb + 1] = fok ? 1 : 0;
                 WSYNC();
-                seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
-            } else if constexpr (KIND == 2) {
-                seg_forward(L, lane, k0, H, xs, true);
+                if (fok) {
+                    seg_acl<true>(L, lane, 0, H);
+                    WSYNC();
+                    seg_forward(L, lane, 0, H, nullptr, true);
+                }
+            }
+            __syncthreads();   // B2
+            if (fb) ok = L.ctrl[kFb + 1] != 0;
+        } else {
+            const bool fb = L.ctrl[kFb] != 0;   // (this IPM iteration's predictor)
+            if (!fb) {
+                if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
+                if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
+            } else if (chain) {
+                seg_vector_backward(L, H, lane, 0, H, true, nullptr);
+                seg_acl<false>(L, lane, 0, H);
+                WSYNC();
+                seg_forward(L, lane, 0, H, nullptr, true);
+            }
+            __syncthreads();   // Bm1
+            if (chain && !fb) seg_chain_vec(L, H, lane);
+            if (a1 > a0 && !fb) seg_acl<false>(L, lane, a0, a1);
+            __syncthreads();   // Bm2: lambda_b, x_w, A'_k[:, CI]
+            if (!fb) {
+                if constexpr (KIND == 1) {
+                    seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
+                    WSYNC();
+                    seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
+                } else if constexpr (KIND == 2) {
+                    seg_forward(L, lane, k0, H, xs, true);
+                }
             }
             __syncthreads();   // B2
         }
@@ -2914,6 +2957,10 @@ struct SqpKernel {
 #pragma unroll
         for (int i = 0; i < NX; ++i) x0[i] = io.x0[(size_t)b * NX + i];
         const int tref = (io.tstep[b] + k) % P.traj_len;
+        // instance solve time (stats slots 10-11), stamped once the instance state is loaded: the stamp
+        // waits in an LDS slot (taken at the kernel's first instruction, or held in registers, it cost the
+        // one-wave kernel 48 B/lane of scratch)
+        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(L.ctrl + kTs) = __builtin_amdgcn_s_memrealtime();
 
         TPHASE(0);
         // ---------------- constraint tightening from the previous solution (gpmpc.py:425-498)
@@ -3261,6 +3308,10 @@ struct SqpKernel {
                 st[7] = max(st[7], (long long)it);
                 st[8] = max(st[8], (long long)qp_total);
                 st[9] += x0_ok ? it + 1 - (lin_hit ? 1 : 0) : 0;   // linearisations computed
+                const long long dt = (long long)(__builtin_amdgcn_s_memrealtime() -
+                                                 *reinterpret_cast<const unsigned long long*>(L.ctrl + kTs));   // 100 MHz ticks
+                st[10] += dt;
+                st[11] = dt;
             }
         }
     }

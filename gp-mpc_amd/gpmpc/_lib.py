@@ -9,13 +9,19 @@ torch device pointers / streams are valid on both sides.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from ctypes import POINTER, c_char_p, c_double, c_int32, c_int64, c_void_p
 from pathlib import Path
 
 import torch  # noqa: F401  (HIP runtime shared with torch)
 
-LIB_PATH = Path(os.environ.get("GPMPC_LIB", Path(__file__).resolve().parent / "lib" / "libgpmpc_mi355x.so"))
+_DEFAULT_LIB = Path(__file__).resolve().parent / "lib" / "libgpmpc_mi355x.so"
+LIB_PATH = Path(os.environ.get("GPMPC_LIB", _DEFAULT_LIB))
+CSRC = Path(__file__).resolve().parents[1] / "csrc"
+# the files gpmpc_build_id's source hash covers, in the Makefile's order (HASHED)
+HASHED = ["sqp_kernel.hip", "gp_kernels.hip", "capi.hip", "gpmpc_common.h", "models.h",
+          "../../include/gpmpc_mi355x.h", "build_id.cpp", "Makefile"]
 
 _lib = None
 
@@ -55,6 +61,7 @@ SIGNATURES = {
     "gpmpc_get_launch_segments": (_I, [_P, _I, POINTER(_I)]),
     "gpmpc_set_tuning": (_I, [_P, _I, _I]),
     "gpmpc_set_cost_buffer": (_I, [_P, _P]),
+    "gpmpc_build_id": (c_char_p, []),
 }
 
 # gpmpc_set_tuning options (include/gpmpc_mi355x.h GPMPC_TUNE_*)
@@ -65,8 +72,35 @@ class GPMPCError(RuntimeError):
     pass
 
 
+def source_hash() -> str:
+    """sha256 (16 hex digits) of the library's sources in this tree, as the Makefile embeds it."""
+    h = hashlib.sha256()
+    for name in HASHED:
+        h.update((CSRC / name).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    """gpmpc_build_id() of the loaded library: 'src=<hash> git=<commit>[+dirty] kind=<product|timing>'."""
+    return load(require_gpu=False).gpmpc_build_id().decode()
+
+
+def build_info() -> dict:
+    """The loaded library's build id, the tree's source hash and whether they match."""
+    bid = build_id()
+    fields = dict(kv.split("=", 1) for kv in bid.split())
+    tree = source_hash()
+    return {"build_id": bid, "lib": str(LIB_PATH), "src_hash_lib": fields.get("src"), "src_hash_tree": tree,
+            "matches_tree": fields.get("src") == tree}
+
+
 def load(require_gpu: bool = True):
-    """Load the HIP library (raises GPMPCError if it is missing; optionally if no GPU)."""
+    """Load the HIP library (raises GPMPCError if it is missing; optionally if no GPU).
+
+    The in-tree library must have been built from the sources next to it: its embedded source hash
+    (gpmpc_build_id) is checked against the tree, so a stale library -- or an A/B variant left in its
+    place -- fails loudly instead of running silently.  A library chosen by GPMPC_LIB (tools' A/B
+    builds) is not checked."""
     global _lib
     if _lib is None:
         if not LIB_PATH.exists():
@@ -76,6 +110,12 @@ def load(require_gpu: bool = True):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if LIB_PATH.resolve() == _DEFAULT_LIB.resolve() and (CSRC / "Makefile").exists():
+            bid = lib.gpmpc_build_id().decode()
+            want = source_hash()
+            if f"src={want} " not in bid + " ":
+                raise GPMPCError(f"stale HIP library {LIB_PATH}: built from sources {bid}, the tree has src={want} "
+                                 "(rebuild: make -C gp-mpc_amd/csrc)")
         _lib = lib
     if require_gpu and not torch.cuda.is_available():
         raise GPMPCError("no HIP device available: the GP-MPC path runs only on the GPU (no CPU fallback)")

@@ -187,7 +187,7 @@ class BatchSolver:
         _lib.check(self.lib.gpmpc_set_tightening(self._h, 1, inverse_cdf(prob, self.nx), Ad.ctypes.data,
                                                  Bd.ctypes.data, K.ctypes.data))
 
-    STATS_SLOTS = 10
+    STATS_SLOTS = 12
 
     def set_stats(self, buf: torch.Tensor | None):
         """Device int64 (B, 10) accumulator of SQP/QP iteration sums, status counts and the

@@ -261,16 +261,25 @@ gpmpc_status gpmpc_set_timing_buffer(gpmpc_handle* h, void* timing_dev);
  * accumulated by the SQP kernel on every gpmpc_solve: [0] SQP iterations, [1] QP (IPM) iterations, [2 + s] number
  * of solves that ended with status s (0..4), [7] largest SQP iteration count of one solve,
  * [8] largest QP iteration total of one solve, [9] linearisations computed (the first SQP
- * iteration of a step reads the stored iterate's linearisation when it is valid).  The caller
+ * iteration of a step reads the stored iterate's linearisation when it is valid), [10] the
+ * instance's solve time inside the SQP kernel in s_memrealtime ticks (the 100 MHz constant clock:
+ * 10 ns; from the instance's first to its last instruction, summed over solves), [11] the last
+ * solve's time in ticks (the slot holds the start stamp while the solve runs).  The slowest instance's time against the kernel's duration is the
+ * latency-bound figure of bench.py's roofline block.  The caller
  * zeroes it; NULL disables (default).  `slots` is the caller's row stride in int64: it must
  * equal GPMPC_STATS_SLOTS (a buffer laid out for another slot count is rejected, not
  * overrun).
  * Replaces reading acados' per-solve "sqp_iter" / "qp_iter" / status stats in a host loop. */
-enum { GPMPC_STATS_SLOTS = 10 };
+enum { GPMPC_STATS_SLOTS = 12 };
 gpmpc_status gpmpc_set_stats_buffer(gpmpc_handle* h, void* stats_dev, int32_t slots);
 
 /* LDS bytes one instance's workgroup needs (capacity planning / tests). */
 int64_t gpmpc_lds_bytes(int32_t model_id, int32_t horizon);
+
+/* Build provenance (host, static string): "src=<sha256 of the library's sources, 16 hex digits>
+ * git=<commit at build time>[+dirty] kind=<product|timing>".  The Python binding recomputes the
+ * source hash from the tree and refuses an in-tree library built from other sources. */
+const char* gpmpc_build_id(void);
 
 #ifdef __cplusplus
 }

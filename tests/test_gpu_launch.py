@@ -26,7 +26,9 @@ def _torch():
 def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
     """all_converge: every instance-step reaches KKT 1e-9 (tools/status_census.py, profiles/r4/
     status_census.jsonl); otherwise the ones stopped at the SQP iteration limit (status 2 on both
-    sides, at most one instance or 5 %) ran the same iterations from the same start and agree to 1e-4."""
+    sides, at most one instance or 5 %) ran the same iterations from the same start and agree to 1e-4.
+    Every instance that converged on both sides is compared first, so a variant that computes
+    something different fails on its trajectories, not only on a borderline status flip."""
     torch = _torch()
     from oracle import cpu_ref
     from gpmpc.solver import BatchSolver
@@ -52,6 +54,10 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
         u0 = ref.step(x0, phase + s, threads=4).copy()
         xg, ug, tg = (t.cpu().numpy() for t in gs.solution())
         st = gs.status.cpu().numpy()
+        both = (st == 0) & (ref.status == 0)
+        ex = np.abs(xg - ref.x).max(axis=(1, 2)) / (1 + np.abs(ref.x).max(axis=(1, 2)))
+        eu = np.abs(ug - ref.u).max(axis=(1, 2)) / (1 + np.abs(ref.u).max(axis=(1, 2)))
+        assert both.any() and max(ex[both].max(), eu[both].max()) <= 1e-6, (s, ex[both], eu[both])
         np.testing.assert_array_equal(st, ref.status)
         ok = st == 0
         if all_converge:
@@ -163,18 +169,37 @@ def test_cost_ordered_dispatch_is_bit_exact():
 
 
 @pytest.mark.parametrize("waves", [2, 4])
-@pytest.mark.parametrize("name,N,H", [("quad2d", 60, 4), ("quad2d", 60, 5), ("quad2d", 60, 7), ("quad2d", 60, 45),
-                                      ("cartpole", 40, 4), ("cartpole", 40, 11), ("cartpole", 40, 40)])
+@pytest.mark.parametrize("name,N,H", [("quad2d", 60, 4), ("quad2d", 60, 5), ("quad2d", 60, 7), ("quad2d", 200, 30),
+                                      ("quad2d", 60, 45), ("cartpole", 40, 4), ("cartpole", 40, 11), ("cartpole", 40, 40)])
 def test_segment_solve_matches_one_segment_recursion(name, N, H, waves):
     """The segment-parallel Newton solve (two segments on two waves, three on four) against the
     same launch shape with one wave running the whole recursion, on the same closed loop at KKT
     1e-9: identical status, x and u within 1e-6 (1 + |.|).  Horizons down to H = 4 (segments of
-    one stage), uneven splits (5, 7, 11) and past the split-lane IPM layout (H = 40, 45)."""
+    one stage), uneven splits (5, 7, 11), the metric's shape (quad2d N = 200, H = 30: what the 2-, 4-
+    and 8-GPU shards run) and past the split-lane IPM layout (H = 40, 45)."""
+    spec, data, hyp = problem(name, N)
+    _seg_vs_one_segment(spec, data, hyp, lqr(spec), H, waves)
+
+
+def test_segment_solve_with_an_unweighted_free_state():
+    """Advisor finding (round 5): the boundary chain inverts M = Ph + Ph W Ph without pivoting, which
+    needs the cost-to-go Ph at the boundary to be positive definite.  With q = 0 on the x position and
+    its bounds at +-1e3 no cost or bound barrier reaches that direction (the position feeds no other
+    state), so Ph is singular up to rounding there.  The chain's pivot check (seg_chain_full, kPivRel)
+    must send such a solve to the one-segment recursion: same status and solution as the launch shape
+    without segments."""
+    spec, data, hyp = problem("quad2d", 60)
+    mats = lqr(spec)   # the tightening's LQR gain from the weighted problem
+    spec.q_diag[0] = 0.0
+    spec.x_lo[0], spec.x_hi[0] = -1e3, 1e3
+    for waves in (2, 4):
+        _seg_vs_one_segment(spec, data, hyp, mats, 30, waves)
+
+
+def _seg_vs_one_segment(spec, data, hyp, mats, H, waves):
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
-    spec, data, hyp = problem(name, N)
-    mats = lqr(spec)
     B, steps = 8, 3
     solvers = []
     for seg in (0, 1):
