@@ -104,7 +104,13 @@ def test_bench_line_contract_on_the_gpu():
     assert abs(out["value"] - 64 * 3 / (out["ms_per_step"] * 3e-3)) <= 1e-6 * out["value"]
     r = out["roofline"]
     assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
-    assert 0.0 < r["achieved"] <= r["achieved_survey_8d"]
+    # SURVEY 8(d)'s count with K_sqp = sqp_iter_mean, over the launch; the executed count beside it
+    assert abs(r["flops_per_launch"] - 64 * out["sqp_iter_mean"] * 480_000) <= 1e-9 * r["flops_per_launch"]
+    assert 0.0 < r["executed"]["achieved"] and r["regime"] == "latency"
+    lat = r["latency"]   # per-instance solve time (s_memrealtime) against the kernel's
+    assert 0.0 < lat["mean_instance_ms_per_step"] <= lat["slowest_instance_ms_per_step"]
+    assert 0.3 < lat["slowest_over_kernel"] <= 1.05, lat
+    assert out["build"]["matches_tree"], out["build"]
     assert len(out["sqp_kernel_ms_per_step_distribution"]["per_step"]) == 3
     assert out["status_counts"]["0"] == 64 * 3
     assert 1.0 <= out["linearisations_per_step"] <= out["sqp_iter_mean"] + 1.0
