@@ -237,6 +237,14 @@ def parse_args(argv=None):
     ap.add_argument("--overlap", type=int, choices=[0, 1], default=None,
                     help="overlapped halves for steps needing more than one round of workgroups "
                          "(gpmpc_set_tuning GPMPC_TUNE_OVERLAP; default: the library's)")
+    ap.add_argument("--lin-cache", type=int, choices=[0, 1], default=None,
+                    help="linearisation cache (gpmpc_set_tuning GPMPC_TUNE_LIN_CACHE; default: the library's)")
+    ap.add_argument("--order", type=int, choices=[0, 1, 2], default=None,
+                    help="cost-ordered dispatch (gpmpc_set_tuning GPMPC_TUNE_ORDER; default: the library's)")
+    ap.add_argument("--var-split", type=int, choices=[0, 1, 4], default=None,
+                    help="triangular variance kernel's column split (gpmpc_set_tuning GPMPC_TUNE_VAR_SPLIT)")
+    ap.add_argument("--waves", type=int, choices=[0, 1, 2, 4], default=None,
+                    help="SQP-kernel waves per instance (gpmpc_set_launch; default 0 = automatic)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
                     help="tightening-variance input map: the reference's (gpmpc.py:437-444) or each GP's own")
     ap.add_argument("--fitc", type=int, default=0, help="FITC mean on M inducing rows (config 5); 0 = exact GP")
@@ -408,6 +416,11 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
             solver.set_tuning(seg=args.seg)
         if args.overlap is not None:
             solver.set_tuning(overlap=args.overlap)
+        for opt in ("lin_cache", "order", "var_split"):
+            if getattr(args, opt) is not None:
+                solver.set_tuning(**{opt: getattr(args, opt)})
+        if args.waves is not None:
+            solver.set_launch(waves=args.waves)
         solver.set_gps(gps, fitc=fitc, variance=args.variance)
         solver.set_tightening(True, 0.95, *lqr_mats)
         solver.reset(reset_iterate=True)

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "gpmpc_common.h"
@@ -86,6 +87,9 @@ struct gpmpc_handle {
     // optional per-kernel HIP-event timing (bench.py's roofline leg)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
+    // whether each profiling event was created fenced (GPMPC_TUNE_EVENT_FENCE at its creation): events
+    // still in ev_var / ev_sqp when the option changes return to the pool later and are dropped there
+    std::unordered_map<hipEvent_t, bool> ev_fenced;
     // (start, end) per launch; a variance launch's end event is also the following SQP launch's
     // start (one event between the two kernels), so the SQP list owns it
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_var, ev_sqp;
@@ -148,16 +152,21 @@ struct StreamMark {
 };
 
 static hipEvent_t take_event(gpmpc_handle* h) {
-    if (!h->ev_pool.empty()) {
+    while (!h->ev_pool.empty()) {
         hipEvent_t e = h->ev_pool.back();
         h->ev_pool.pop_back();
-        return e;
+        const auto it = h->ev_fenced.find(e);
+        if (it != h->ev_fenced.end() && it->second == h->event_fence) return e;
+        // created under the other GPMPC_TUNE_EVENT_FENCE setting: an A/B run must not mix them
+        if (it != h->ev_fenced.end()) h->ev_fenced.erase(it);
+        (void)hipEventDestroy(e);
     }
     hipEvent_t e = nullptr;
     // timing-only events: no system-scope fence (cache writeback / invalidate) when recorded,
     // which otherwise adds ~5 us of dispatch gap around every kernel it brackets
     const unsigned flags = h->event_fence ? hipEventDefault : hipEventDisableSystemFence;
     if (hipEventCreateWithFlags(&e, flags) != hipSuccess) return nullptr;
+    h->ev_fenced[e] = h->event_fence;
     return e;
 }
 
@@ -865,8 +874,11 @@ gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value) {
             return GPMPC_OK;
         case GPMPC_TUNE_EVENT_FENCE:
             if (value != 0 && value != 1) break;
-            if (h->event_fence != (value == 1)) {   // pooled events carry the old flags
-                for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+            if (h->event_fence != (value == 1)) {   // pooled events carry the old flags (the ones still in
+                for (hipEvent_t e : h->ev_pool) {     // use are dropped when they come back: take_event)
+                    h->ev_fenced.erase(e);
+                    (void)hipEventDestroy(e);
+                }
                 h->ev_pool.clear();
             }
             h->event_fence = value == 1;

@@ -27,6 +27,10 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
+#ifndef GPMPC_WSPL_SEG   // (round-6 A/B of kWsplSeg: tools/build_variant.sh with -DGPMPC_WSPL_SEG=0)
+#define GPMPC_WSPL_SEG 1
+#endif
+
 namespace gpmpc {
 
 // Orders the LDS traffic of the (main) wave.  One wave per block: __syncthreads.  With GP helper
@@ -620,6 +624,7 @@ struct SqpKernel {
     // the same way.  The stage operands (one G' row, one K' row per lane) are loaded a stage ahead.
     // Output: dxv.
     __device__ static void valu_forward_big(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         const int row = lane < NX ? lane : 0;
         const int a = (lane >= NX && lane < NB) ? lane - NX : 0;
         const double* gp = L.G + (size_t)row * GS;
@@ -678,6 +683,7 @@ struct SqpKernel {
     // with pv and gu broadcast by v_readlane.  Outputs: p in P', kff in K'.
     // Scratch: t aliases hq (rewritten before the next factorisation).
     __device__ static void valu_vector_big(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         double* T = L.hq;
         const int n = H * NX;
         auto t_entry = [&](int e) {
@@ -757,6 +763,7 @@ struct SqpKernel {
 
     // Per-lane step of stage k from the Riccati solution: dd = [dx_k; du_k] and dpi_k.
     __device__ static void recover_step(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        lane = phase_lane(lane);
         const bool on = lane <= H;
         double dx[NX], dxn[NX];
 #pragma unroll
@@ -814,6 +821,7 @@ struct SqpKernel {
     // lane move.  Stores of stage k are issued after stage k-1's W' products (sched_barrier), off
     // the chain.  Outputs: packed P', K' = [K | kff], Ru^-1 per stage.
     __device__ static bool mfma_backward_h(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         const int lr = lane >> 4, lc = lane & 15;
         constexpr int CI = NX, UI = 8;
         static_assert(NX + 1 <= 8 && NU <= 2 && UI + NU <= 16, "homogeneous tile layout");
@@ -899,7 +907,6 @@ struct SqpKernel {
         double* srui = rst ? L.Rui + (size_t)(H - 1) * NU * NU + lane : L.dummy;
         const int srui_st = rst ? NU * NU : 0;
         double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
-        bool pend = false;
         auto flush = [&]() {
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
@@ -911,16 +918,14 @@ struct SqpKernel {
             *srui = pend_r;
             srui -= srui_st;
         };
-        auto flush_at = [&]() {   // the previous stage's stores, pinned after the W' products
-            __builtin_amdgcn_sched_barrier(0);
-            if (pend) flush();
-            __builtin_amdgcn_sched_barrier(0);
-            pend = true;
-        };
-        auto stage = [&](const Stage& sd) {
+        // fl: the previous stage's stores are pending (every stage but the first, which is peeled off the
+        // loop: no branch inside the stage); issued after this stage's W' products, off the chain
+        auto stage = [&](const Stage& sd, auto fl) {
             f64x4 w = mfma64(pn[0], sd.g[0], f64x4{0.0, 0.0, 0.0, 0.0});
             w = mfma64(pn[1], sd.g[1], w);
-            flush_at();
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (decltype(fl)::value) flush();
+            __builtin_amdgcn_sched_barrier(0);
             f64x4 m = mfma64(sd.g[0], w[0], f64x4{sd.d[0], sd.d[1], sd.d[2], 0.0});
             m = mfma64(sd.g[1], w[1], m);
             double Ru[NU][NU];
@@ -966,14 +971,16 @@ struct SqpKernel {
         };
         Stage s0, s1;
         load_stage(s0);
-        int k = H - 1;
+        load_stage(s1);
+        stage(s0, std::false_type{});
+        int k = H - 2;
         for (; k >= 1; k -= 2) {
-            load_stage(s1);
-            stage(s0);
-            if (k >= 2) load_stage(s0);
-            stage(s1);
+            load_stage(s0);
+            stage(s1, std::true_type{});
+            load_stage(s1);   // (past stage 0 on the last pass: the zero / previous slots, never used)
+            stage(s0, std::true_type{});
         }
-        if (k == 0) stage(s0);
+        if (k == 0) stage(s1, std::true_type{});
         flush();
         return ok;
     }
@@ -990,6 +997,7 @@ struct SqpKernel {
     // right-hand side of K'.  Outputs as mfma_backward_h (packed P', K', Ru^-1).
     static constexpr bool kMfmaBig = !kMfma && NX <= 12 && NX + 1 <= 16 && NU == 4;
     __device__ static bool mfma_backward_big(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         if constexpr (!kMfmaBig) {
             return false;
         } else {
@@ -1159,6 +1167,7 @@ struct SqpKernel {
     // affine column when the factorisation is unchanged (corrector).
     template <bool full>
     __device__ static void acl_phase(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         if constexpr (full) {
             // one row (k, i) of A'_k per lane and pass: the G'_k row and K'_k are contiguous reads,
             // the PS outputs one contiguous store
@@ -1251,6 +1260,7 @@ struct SqpKernel {
     // LDS zero slot (stride 0) and the homogeneous corner the one slot, so the stage operand is one
     // unconditional load issued a stage ahead.
     __device__ static void mfma4_forward(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         static_assert(NX >= 4 && NX + 1 <= 8, "homogeneous 8-vector");
         {
             const Mfma4Lane q = mfma4_lane(lane);
@@ -1283,6 +1293,7 @@ struct SqpKernel {
     // stage, mfma4_stage); t_k = P_{k+1} c_k and vt_k are built for all stages in parallel.
     // Scratch: t aliases hq (rewritten before the next factorisation), vt aliases dxv.
     __device__ static void mfma4_vector_backward(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         double* T = L.hq;
         double* VT = L.dxv;
         // entries (k, i) two per pass, both computed before either is stored (T and VT alias other
@@ -1414,6 +1425,7 @@ struct SqpKernel {
 
     // Per-lane step from the MFMA Riccati solution (packed P').
     __device__ static void recover_step_mfma(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        lane = phase_lane(lane);
         const bool on = lane <= H;
         const int kk = min(lane, H - 1);
         double dx[NX], dxn[NX];
@@ -1453,74 +1465,117 @@ struct SqpKernel {
     // the dense KKT solve).
     __host__ __device__ static int seg_start(int w, int H) { return (w * H) / NSEG; }
     __device__ static int lam_of(int t) { return (t >= LI && t < LI + NX) ? t - LI : -1; }
+    // Every Newton-solve phase starts from an opaque copy of its lane index, so the lane-derived LDS
+    // addresses of the phase are recomputed there (a few VALU operations) instead of hoisted out of the
+    // SQP loop, held across the IPM and spilled to AGPRs / scratch (reloaded with a memory latency per
+    // phase).  Round 6: the quad2d / cartpole kernels' scratch 112-208 B/lane -> 0.
+    __device__ static int phase_lane(int lane) {
+        asm volatile("" : "+v"(lane));
+        return lane;
+    }
+    // P_x,lambda of stage k of a lambda segment (in its P' block)
+    __device__ static double* pxl_at(const Lds& L, int k) { return L.P + (size_t)k * PPB + PXL; }
 
-    // Riccati factorisation of stages k0 .. k1-1, mfma_backward_h's stage.  AUG (segment A): over
-    // z = [x; 1; lambda] from the terminal cost lambda' x_k1; else (segment B, k1 = H) from the true P'_H.
-    // The lambda blocks add no MFMA to the stage: the lambda rows of G'' are the identity, so
-    //   W' = P' G''          = P'[:, 0..7] G''[0..7, :] + (P' on the lambda columns)   C-init of W's first MFMA
-    //   M' = G''^T W' + D    = G''[0..7, :]^T W'[0..7, :] + (W' on the lambda rows, D elsewhere)
-    // and the Schur MFMA P'_k = M' + M'_{.u} K' covers all 16 columns (K_lambda rides in K').  Stores per
-    // stage: packed P and p (AUG: + P_x,lambda at PXL), K' = [K | kff (| K_lambda)], Ru^-1; AUG: the
-    // stage-k0 tile V (row-major 16 x 16) into the boundary data.
     template <bool AUG>
-    __device__ static bool seg_factor(const Lds& L, int H, int lane, int k0, int k1, double* vtile) {
-        const int lr = lane >> 4, lc = lane & 15;
-        constexpr int CI = NX, UI = 8, NR = AUG ? 4 : 2;
+    struct Fac {
+        static constexpr int CI = NX, UI = 8, NR = AUG ? 4 : 2;
         static_assert(NX + 1 <= 8 && NU <= 2 && UI + NU <= 16, "homogeneous tile layout");
-        auto gcol = [](int t) { return t < NX ? t : (t == CI ? NB : ((t >= UI && t < UI + NU) ? NX + t - UI : -1)); };
-        auto svar = [](int t) { return t < NX ? t : ((t >= UI && t < UI + NU) ? NX + t - UI : -1); };
-        const int gc_lc = gcol(lc), sv_lc = svar(lc), lm_lc = AUG ? lam_of(lc) : -1;
+        struct Stage { double g[2], d[3]; };
         double pn[NR];
+        // G'' rows 4s + lr, column lc: LDS streams (masked lanes read the zero / one slots, stride 0)
+        const double* pg[2];
+        int gst[2];
+        const double* pd[3];
+        int dst[3];
+        double* sp[2];
+        int sp_st[2];
+        double* sk;
+        int sk_st;
+        double* srui;
+        int srui_st;
+        bool lamc, lam2, lam3;
+        double pend_p[2], pend_k, pend_r;   // the last stage's stores, issued during the next stage
+        bool ok;
+        int lr, lc, lane;
+
+        __device__ static int gcol(int t) { return t < NX ? t : (t == CI ? NB : ((t >= UI && t < UI + NU) ? NX + t - UI : -1)); }
+        __device__ static int svar(int t) { return t < NX ? t : ((t >= UI && t < UI + NU) ? NX + t - UI : -1); }
+
+        // stages k0 .. k1-1, backward; AUG: from lambda' x_k1, else from the true P'_H (k1 = H)
+        __device__ void init(const Lds& L, int H, int ln, int k0, int k1) {
+            (void)k0;
+            lane = phase_lane(ln);
+            lr = lane >> 4;
+            lc = lane & 15;
+            const int gc_lc = gcol(lc), sv_lc = svar(lc), lm_lc = AUG ? lam_of(lc) : -1;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int t = lr + 4 * r;
-            double v = 0.0;
-            if constexpr (AUG) {   // lambda' x_k1: P'[x_i][lambda_i] = P'[lambda_i][x_i] = 1
-                v = ((t < NX && lm_lc == t) || (lam_of(t) >= 0 && lam_of(t) == lc)) ? 1.0 : 0.0;
-            } else {               // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
-                if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NBS + t] : 0.0;
-                else if (t < NX && lc == CI) v = L.gq[H * NBS + t];
-                else if (t == CI && lc < NX) v = L.gq[H * NBS + lc];
+            for (int r = 0; r < NR; ++r) {
+                const int t = lr + 4 * r;
+                double v = 0.0;
+                if constexpr (AUG) {   // lambda' x_k1: P'[x_i][lambda_i] = P'[lambda_i][x_i] = 1
+                    v = ((t < NX && lm_lc == t) || (lam_of(t) >= 0 && lam_of(t) == lc)) ? 1.0 : 0.0;
+                } else {               // P'_H: diag(hq_H[x]), gq_H[x] in row and column CI
+                    if (t < NX && lc < NX) v = (t == lc) ? L.hq[H * NBS + t] : 0.0;
+                    else if (t < NX && lc == CI) v = L.gq[H * NBS + t];
+                    else if (t == CI && lc < NX) v = L.gq[H * NBS + lc];
+                }
+                pn[r] = v;
             }
-            pn[r] = v;
-        }
-        if constexpr (!AUG) {   // P'_H (packed) for the multiplier recovery of stage H-1
-            double* PH = L.P + (size_t)H * PPB;
+            if constexpr (!AUG) {   // P'_H (packed) for the multiplier recovery of stage H-1
+                double* PH = L.P + (size_t)H * PPB;
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int t = lr + 4 * r;
+                    if (t < NX) {
+                        if (lc == CI) PH[PO + t] = pn[r];
+                        else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
+                    }
+                }
+            }
+            ok = true;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int t = lr + 4 * s2;
+                const bool ld = t < NX && gc_lc >= 0;
+                const bool one = t == CI && lc == CI;
+                pg[s2] = ld ? L.G + (size_t)(k1 - 1) * NX * GS + t * GS + gc_lc : L.zero + (one ? 7 : 0);
+                gst[s2] = ld ? NX * GS : 0;
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const int t = lr + 4 * r, sv_t = svar(t);
+                const double* base = L.zero;
+                bool on = false;
+                if (sv_t >= 0 && t == lc) { base = L.hq + sv_t; on = true; }
+                else if (sv_t >= 0 && lc == CI) { base = L.gq + sv_t; on = true; }
+                else if (t == CI && sv_lc >= 0) { base = L.gq + sv_lc; on = true; }
+                pd[r] = on ? base + (size_t)(k1 - 1) * NBS : L.zero;
+                dst[r] = on ? NBS : 0;
+            }
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 const int t = lr + 4 * r;
-                if (t < NX) {
-                    if (lc == CI) PH[PO + t] = pn[r];
-                    else if (lc < NX && t <= lc) PH[pidx(t, lc)] = pn[r];
-                }
+                const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc) || lm_lc >= 0);
+                const int idx = (lc == CI) ? PO + t
+                                           : (lm_lc >= 0 ? PXL + t * NX + lm_lc : pidx(t < lc ? t : lc, t < lc ? lc : t));
+                sp[r] = st ? L.P + (size_t)(k1 - 1) * PPB + idx : L.dummy;
+                sp_st[r] = st ? PPB : 0;
             }
+            const int kcol = lc < NX ? lc : (lc == CI ? NX : (lm_lc >= 0 ? NX + 1 + lm_lc : -1));
+            const bool kst = lr < NU && kcol >= 0;
+            sk = kst ? L.K + (size_t)(k1 - 1) * NU * KST + lr * KST + kcol : L.dummy;
+            sk_st = kst ? NU * KST : 0;
+            const bool rst = lane < NU * NU;
+            srui = rst ? L.Rui + (size_t)(k1 - 1) * NU * NU + lane : L.dummy;
+            srui_st = rst ? NU * NU : 0;
+            // C-init masks of the lambda blocks: columns (W') and rows of elements 2, 3 (M')
+            lamc = lm_lc >= 0;
+            lam2 = AUG && lam_of(lr + 8) >= 0;
+            lam3 = AUG && lam_of(lr + 12) >= 0;
+            pend_p[0] = pend_p[1] = pend_k = pend_r = 0.0;
         }
-        bool ok = true;
-        const double* pg[2];
-        int gst[2];
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const int t = lr + 4 * s2;
-            const bool ld = t < NX && gc_lc >= 0;
-            const bool one = t == CI && lc == CI;
-            pg[s2] = ld ? L.G + (size_t)(k1 - 1) * NX * GS + t * GS + gc_lc : L.zero + (one ? 7 : 0);
-            gst[s2] = ld ? NX * GS : 0;
-        }
-        const double* pd[3];
-        int dst[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int t = lr + 4 * r, sv_t = svar(t);
-            const double* base = L.zero;
-            bool on = false;
-            if (sv_t >= 0 && t == lc) { base = L.hq + sv_t; on = true; }
-            else if (sv_t >= 0 && lc == CI) { base = L.gq + sv_t; on = true; }
-            else if (t == CI && sv_lc >= 0) { base = L.gq + sv_lc; on = true; }
-            pd[r] = on ? base + (size_t)(k1 - 1) * NBS : L.zero;
-            dst[r] = on ? NBS : 0;
-        }
-        struct Stage { double g[2], d[3]; };
-        auto load_stage = [&](Stage& st) {
+        __device__ void load(const Lds& L, Stage& st) {
+            (void)L;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 st.g[q] = *pg[q];
@@ -1531,31 +1586,8 @@ struct SqpKernel {
                 st.d[q] = *pd[q];
                 pd[q] -= dst[q];
             }
-        };
-        double* sp[2];
-        int sp_st[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int t = lr + 4 * r;
-            const bool st = t < NX && ((lc == CI) || (lc < NX && t <= lc) || lm_lc >= 0);
-            const int idx = (lc == CI) ? PO + t
-                                       : (lm_lc >= 0 ? PXL + t * NX + lm_lc : pidx(t < lc ? t : lc, t < lc ? lc : t));
-            sp[r] = st ? L.P + (size_t)(k1 - 1) * PPB + idx : L.dummy;
-            sp_st[r] = st ? PPB : 0;
         }
-        const int kcol = lc < NX ? lc : (lc == CI ? NX : (lm_lc >= 0 ? NX + 1 + lm_lc : -1));
-        const bool kst = lr < NU && kcol >= 0;
-        double* sk = kst ? L.K + (size_t)(k1 - 1) * NU * KST + lr * KST + kcol : L.dummy;
-        const int sk_st = kst ? NU * KST : 0;
-        const bool rst = lane < NU * NU;
-        double* srui = rst ? L.Rui + (size_t)(k1 - 1) * NU * NU + lane : L.dummy;
-        const int srui_st = rst ? NU * NU : 0;
-        // C-init masks of the lambda blocks: columns (W') and rows of elements 2, 3 (M')
-        const bool lamc = lm_lc >= 0;
-        const bool lam2 = AUG && lam_of(lr + 8) >= 0, lam3 = AUG && lam_of(lr + 12) >= 0;
-        double pend_p[2] = {0.0, 0.0}, pend_k = 0.0, pend_r = 0.0;
-        bool pend = false;
-        auto flush = [&]() {
+        __device__ void flush() {   // the previous stage's stores
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
                 *sp[r] = pend_p[r];
@@ -1565,29 +1597,28 @@ struct SqpKernel {
             sk -= sk_st;
             *srui = pend_r;
             srui -= srui_st;
-        };
-        auto flush_at = [&]() {
-            __builtin_amdgcn_sched_barrier(0);
-            if (pend) flush();
-            __builtin_amdgcn_sched_barrier(0);
-            pend = true;
-        };
-        auto stage = [&](const Stage& sd) {
+        }
+        // W' = P' G'' (2 chained MFMAs; AUG: P's lambda columns as the C-init)
+        __device__ f64x4 wprod(const Stage& sd) const {
             f64x4 cw = {0.0, 0.0, 0.0, 0.0};
             if constexpr (AUG) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) cw[r] = lamc ? pn[r] : 0.0;
             }
             f64x4 w = mfma64(pn[0], sd.g[0], cw);
-            w = mfma64(pn[1], sd.g[1], w);
-            flush_at();
+            return mfma64(pn[1], sd.g[1], w);
+        }
+        // C-init of M' = G''^T W' + D (AUG: W's lambda rows)
+        __device__ f64x4 mcinit(const Stage& sd, const f64x4& w) const {
             f64x4 cm = {sd.d[0], sd.d[1], sd.d[2], 0.0};
             if constexpr (AUG) {
                 cm[2] = lam2 ? w[2] : sd.d[2];
                 cm[3] = lam3 ? w[3] : 0.0;
             }
-            f64x4 m = mfma64(sd.g[0], w[0], cm);
-            m = mfma64(sd.g[1], w[1], m);
+            return cm;
+        }
+        // Ru = M'_uu (readlane), K' = -Ru^-1 M'_u. (adjugate / cubic reciprocal), Schur MFMA P'_k = M' + M'_.u K'
+        __device__ void finish(const f64x4& m) {
             double Ru[NU][NU];
 #pragma unroll
             for (int a = 0; a < NU; ++a)
@@ -1627,29 +1658,62 @@ struct SqpKernel {
             pend_r = rv;
 #pragma unroll
             for (int r = 0; r < NR; ++r) pn[r] = pk[r];
-        };
-        Stage s0, s1;
-        load_stage(s0);
-        int k = k1 - 1;
-        for (; k >= k0 + 1; k -= 2) {
-            load_stage(s1);
-            stage(s0);
-            if (k >= k0 + 2) load_stage(s0);
-            stage(s1);
         }
-        if (k == k0) stage(s0);
-        flush();
-        if constexpr (AUG) {
+        // one stage; the previous stage's stores (FL: there is one) issued after this stage's W' products,
+        // off the chain
+        template <bool FL>
+        __device__ void stage(const Stage& sd) {
+            const f64x4 w = wprod(sd);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (FL) flush();
+            __builtin_amdgcn_sched_barrier(0);
+            f64x4 m = mfma64(sd.g[0], w[0], mcinit(sd, w));
+            m = mfma64(sd.g[1], w[1], m);
+            finish(m);
+        }
+        // AUG: the stage-k0 tile V (row-major 16 x 16) into the boundary data
+        __device__ void store_tile(double* vtile) const {
+            if constexpr (AUG) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) vtile[(lr + 4 * r) * 16 + lc] = pn[r];
+                for (int r = 0; r < 4; ++r) vtile[(lr + 4 * r) * 16 + lc] = pn[r];
+            }
         }
-        return ok;
+    };
+
+    // Riccati factorisation of stages k0 .. k1-1, mfma_backward_h's stage.  AUG (segment A): over
+    // z = [x; 1; lambda] from the terminal cost lambda' x_k1; else (segment B, k1 = H) from the true P'_H.
+    // The lambda blocks add no MFMA to the stage: the lambda rows of G'' are the identity, so
+    //   W' = P' G''          = P'[:, 0..7] G''[0..7, :] + (P' on the lambda columns)   C-init of W's first MFMA
+    //   M' = G''^T W' + D    = G''[0..7, :]^T W'[0..7, :] + (W' on the lambda rows, D elsewhere)
+    // and the Schur MFMA P'_k = M' + M'_{.u} K' covers all 16 columns (K_lambda rides in K').  Stores per
+    // stage: packed P and p (AUG: + P_x,lambda at PXL), K' = [K | kff (| K_lambda)],
+    // Ru^-1; AUG: the stage-k0 tile V (row-major 16 x 16) into the boundary data.
+    template <bool AUG>
+    __device__ static bool seg_factor(const Lds& L, int H, int lane, int k0, int k1, double* vtile) {
+        Fac<AUG> f;
+        f.init(L, H, lane, k0, k1);
+        typename Fac<AUG>::Stage s0, s1;
+        f.load(L, s0);
+        f.load(L, s1);
+        f.template stage<false>(s0);   // (the first stage has no stores pending)
+        int k = k1 - 2;
+        for (; k >= k0 + 1; k -= 2) {
+            f.load(L, s0);
+            f.template stage<true>(s1);
+            f.load(L, s1);   // (past stage k0 on the last pass: loaded, never used)
+            f.template stage<true>(s0);
+        }
+        if (k == k0) f.template stage<true>(s1);
+        f.flush();
+        f.store_tile(vtile);
+        return f.ok;
     }
 
     // Closed-loop stage maps A'_k = [A + B K | B kff + c] of stages k0 .. k1-1 (acl_phase over a range,
     // K' row stride KST); only the affine column when the feedback is unchanged.
     template <bool full>
     __device__ static void seg_acl(const Lds& L, int lane, int k0, int k1) {
+        lane = phase_lane(lane);
         if constexpr (full) {
             for (int e = k0 * NX + lane; e < k1 * NX; e += 64) {
                 const int k = e / NX, i = e - k * NX;
@@ -1700,6 +1764,7 @@ struct SqpKernel {
     // Forward sweep of stages k0 .. k1-1 from dx_k0 = xs (NULL: 0), mfma4_forward over a range; dx_k0 is
     // stored, dx_k1 only when store_end (segment A leaves x_SM to segment B, which starts from it).
     __device__ static void seg_forward(const Lds& L, int lane, int k0, int k1, const double* xs, bool store_end) {
+        lane = phase_lane(lane);
         const Mfma4Lane q = mfma4_lane(lane);
         const bool ld = q.row < NX && q.col <= NX;
         const double* src = ld ? L.Acl + (size_t)k0 * NX * PS + q.row * PS + q.col
@@ -1729,6 +1794,7 @@ struct SqpKernel {
     // (segment B): from the true p_H; else (segment A) from the zero terminal P_k1 = 0, p_k1 = 0, plus
     // V_lambda,1 = sum_k P_lambda,x,k+1 (c_k + B_k kff_k) (P_lambda,x,k1 = I) into the boundary data.
     __device__ static void seg_vector_backward(const Lds& L, int H, int lane, int k0, int k1, bool last, double* vl1) {
+        lane = phase_lane(lane);
         double* T = L.hq;
         double* VT = L.dxv;
         const int n = k1 * NX;
@@ -1856,48 +1922,54 @@ struct SqpKernel {
             L.K[(size_t)k * NU * KST + a * KST + NX] = -kf;
         }
         WSYNC();
-        if (!last) {
-            // V_lambda,1 = sum_k P_lambda,x,k+1 z_k with z_k = c_k + B_k kff_k (this pass's kff, formed
-            // here: the closed-loop maps' affine columns follow during the chain, seg_part): lane (k, j)
-            // forms term j of stage k into VT (its p-recurrence input is consumed), then lanes j < NX add
-            // the terms
-            for (int e = k0 * NX + lane; e < n; e += 64) {
-                const int k = e / NX, j = e - k * NX;
-                const double* G = L.G + (size_t)k * NX * GS;
-                const double* Kk = L.K + (size_t)k * NU * KST + NX;
-                const double* Pl = L.P + (size_t)(k + 1) * PPB + PXL;
-                // every load first (before a scheduling barrier); P_lambda,x,k1 = I at the segment end, the
-                // P' load unconditional (bsel: a ternary would sink it into a branch with a wait per term)
-                double kf[NU], gc[NX], gu[NX][NU], pl[NX];
+        if (!last) seg_vl1(L, lane, k0, k1, vl1);
+    }
+
+    // V_lambda,1 = sum_k P_lambda,x,k+1 z_k of a lambda segment k0 .. k1-1 (its corrector pass), into vl1
+    __device__ static void seg_vl1(const Lds& L, int lane, int k0, int k1, double* vl1) {
+        lane = phase_lane(lane);
+        double* VT = L.dxv;
+        const int n = k1 * NX;
+        // V_lambda,1 = sum_k P_lambda,x,k+1 z_k with z_k = c_k + B_k kff_k (this pass's kff, formed
+        // here: the closed-loop maps' affine columns follow during the chain, seg_part): lane (k, j)
+        // forms term j of stage k into VT (its p-recurrence input is consumed), then lanes j < NX add
+        // the terms
+        for (int e = k0 * NX + lane; e < n; e += 64) {
+            const int k = e / NX, j = e - k * NX;
+            const double* G = L.G + (size_t)k * NX * GS;
+            const double* Kk = L.K + (size_t)k * NU * KST + NX;
+            const double* Pl = pxl_at(L, k + 1);
+            // every load first (before a scheduling barrier); P_lambda,x,k1 = I at the segment end, the
+            // P' load unconditional (bsel: a ternary would sink it into a branch with a wait per term)
+            double kf[NU], gc[NX], gu[NX][NU], pl[NX];
 #pragma unroll
-                for (int a = 0; a < NU; ++a) kf[a] = Kk[a * KST];
+            for (int a = 0; a < NU; ++a) kf[a] = Kk[a * KST];
 #pragma unroll
-                for (int t = 0; t < NX; ++t) {
-                    gc[t] = G[t * GS + NB];
-                    pl[t] = Pl[t * NX + j];
+            for (int t = 0; t < NX; ++t) {
+                gc[t] = G[t * GS + NB];
+                pl[t] = Pl[t * NX + j];
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) gu[t][a] = G[t * GS + NX + a];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                const unsigned mend = (k + 1 == k1) ? 0xffffffffu : 0u;
-                double acc = 0.0;
-#pragma unroll
-                for (int t = 0; t < NX; ++t) {
-                    double z = gc[t];
-#pragma unroll
-                    for (int a = 0; a < NU; ++a) z = fma(gu[t][a], kf[a], z);
-                    acc = fma(bsel(mend, t == j ? 1.0 : 0.0, pl[t]), z, acc);
-                }
-                VT[e] = acc;
+                for (int a = 0; a < NU; ++a) gu[t][a] = G[t * GS + NX + a];
             }
-            WSYNC();
-            if (lane < NX) {
-                double acc = 0.0;
-                for (int k = k0; k < k1; ++k) acc += VT[k * NX + lane];
-                vl1[lane] = acc;
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned mend = (k + 1 == k1) ? 0xffffffffu : 0u;
+            double acc = 0.0;
+#pragma unroll
+            for (int t = 0; t < NX; ++t) {
+                double z = gc[t];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) z = fma(gu[t][a], kf[a], z);
+                acc = fma(bsel(mend, t == j ? 1.0 : 0.0, pl[t]), z, acc);
             }
-            WSYNC();
+            VT[e] = acc;
         }
+        WSYNC();
+        if (lane < NX) {
+            double acc = 0.0;
+            for (int k = k0; k < k1; ++k) acc += VT[k * NX + lane];
+            vl1[lane] = acc;
+        }
+        WSYNC();
     }
 
     // Boundary chain of the predictor (wave 1, after every segment's factorisation).  Backward over the
@@ -1920,6 +1992,7 @@ struct SqpKernel {
     // fallback), which never inverts Ph.
     static constexpr double kPivRel = 1e-12;
     __device__ static bool seg_chain_full(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         constexpr int CI = NX;
         const int c = min(lane, 3 * NX);
         const int cm = min(c, NX - 1);
@@ -2029,6 +2102,7 @@ struct SqpKernel {
     // boundary data.  V_l1 is the tile's affine column after a factorisation, the corrector's vector
     // pass result (SB_VL1) after a vector pass (vec).
     __device__ static void seg_chain_forward(const Lds& L, int lane, bool vec) {
+        lane = phase_lane(lane);
         constexpr int CI = NX;
         const int i = min(lane, NX - 1);
         double xh[NX];
@@ -2086,6 +2160,7 @@ struct SqpKernel {
     // V_l1 and V_x1 (the segment's zero-terminal p at its start) from the others':
     //   y_b = T_b^-1 (Ph V_l1 + ph),  ph <- V_x1 + V_xl y_b,  then seg_chain_forward.
     __device__ static void seg_chain_vec(const Lds& L, int H, int lane) {
+        lane = phase_lane(lane);
         const int i = min(lane, NX - 1);
         // every load first (before a scheduling barrier), the stores after the recursion
         double phv = L.P[(size_t)seg_start(NSEG - 1, H) * PPB + PO + i];
@@ -2139,6 +2214,7 @@ struct SqpKernel {
     // rewrites both); the closed-loop affine column A'_k[:, CI] = c_k + B_k kff_k follows in the same
     // pass (+ B_k K_lambda,k lambda), so no closed-loop pass runs between the fold and the sweep.
     __device__ static void seg_fold(const Lds& L, int lane, int k0, int k1, const double* lamp) {
+        lane = phase_lane(lane);
         double lam[NX];
 #pragma unroll
         for (int j = 0; j < NX; ++j) lam[j] = lamp[j];
@@ -2158,7 +2234,7 @@ struct SqpKernel {
                 for (int j = 0; j < NX; ++j) kl[a][j] = Kk[a * KST + NX + 1 + j];
             }
 #pragma unroll
-            for (int j = 0; j < NX; ++j) pxl[j] = Pk[PXL + i * NX + j];
+            for (int j = 0; j < NX; ++j) pxl[j] = pxl_at(L, k)[i * NX + j];
             double ac = L.Acl[(size_t)k * NX * PS + i * PS + NX];
             double pv = Pk[PO + i];
             const double kv = *kp;
@@ -2184,6 +2260,7 @@ struct SqpKernel {
     // Per-lane step from the segment-parallel solution: recover_step_mfma with the KST / PPB strides (the
     // boundary costate is already folded into segment A's kff and p, seg_fold).
     __device__ static void recover_step_seg(const Lds& L, int H, int lane, double (&dd)[NB], double (&dpi)[NX]) {
+        lane = phase_lane(lane);
         const bool on = lane <= H;
         const int kk = min(lane, H - 1);
         double dx[NX], dxn[NX];
@@ -2336,6 +2413,14 @@ struct SqpKernel {
         constexpr int sg0 = seg_of_wave(0);
         return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd);
     }
+    // kWsplSeg: every wave is inside qp_ipm and runs its own part (the IPM's block barrier before the call
+    // stands for B1)
+    __device__ static bool seg_all(const Lds& L, int H, int lane, int w, int cmd) {
+        const int sg = seg_of_wave(w);
+        if (sg == NSEG - 1) return seg_part<2>(L, H, lane, w, sg, w == 1, cmd);
+        if (sg >= 0) return seg_part<1>(L, H, lane, w, sg, w == 1, cmd);
+        return seg_part<0>(L, H, lane, w, 0, false, cmd);
+    }
     // helper wave w's part of a segment command (after B1)
     __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
         const int sg = seg_of_wave(w);
@@ -2457,10 +2542,14 @@ struct SqpKernel {
     // NV variables' IPM state (the unsplit layout spilled 3.5 KB per lane to scratch at H = 40).  The
     // full step vector for the dynamics residual, the reductions and the Riccati status cross the
     // waves through LDS at block barriers; the Riccati recursion runs on wave 0.
-    // (the single-tile models keep their two-lanes-per-stage split on wave 0 when they run four waves:
-    // their helpers take the GP tile passes only -- sharing the IPM's elementwise work costs more in
-    // cross-wave reductions than it saves at NB <= 8)
-    static constexpr bool WSPL = NWAVES > 1 && !kMfma;
+    // The single-tile models on four waves with the segment solve (round 6, kWsplSeg) split the same way:
+    // wave w holds variables 2w, 2w + 1 of every stage (NV = 2 against the two-lanes-per-stage split's 4
+    // on wave 0), and every wave calls the segment solve itself (seg_all) instead of wave 0 posting it.
+    // Without the segment solve, and on two waves (NV = 4 either way), they keep the SPL split on wave 0:
+    // there the helpers take the GP tile passes only (round 3 measured the cross-wave reductions costlier
+    // than the elementwise work they share at NB <= 8 while wave 0 also ran the whole recursion).
+    static constexpr bool kWsplSeg = GPMPC_WSPL_SEG && kSeg && NWAVES == 4;
+    static constexpr bool WSPL = NWAVES > 1 && (!kMfma || kWsplSeg);
     // (WSPL: NWAVES NV may exceed NB -- cartpole's 5 variables in slots of 2 -- and the slots past NB
     // are inactive: never stored, never published)
     template <bool SPL>
@@ -2671,8 +2760,10 @@ struct SqpKernel {
                 TPHASE(4);
                 double dd[NV], dp[NX];
                 if constexpr (kSeg) {
-                    // segment-parallel solve on the helper waves (seg_run)
-                    const bool rok = seg_run(L, H, lane, kCmdSegFactor);
+                    // segment-parallel solve: posted to the helper waves (seg_run), or every wave's own part (WSPL)
+                    bool rok;
+                    if constexpr (WSPL) rok = seg_all(L, H, lane, wv, kCmdSegFactor);
+                    else rok = seg_run(L, H, lane, kCmdSegFactor);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
@@ -2753,7 +2844,8 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(5);
                 if constexpr (kSeg) {
-                    (void)seg_run(L, H, lane, kCmdSegVector);
+                    if constexpr (WSPL) (void)seg_all(L, H, lane, wv, kCmdSegVector);
+                    else (void)seg_run(L, H, lane, kCmdSegVector);
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
@@ -3476,7 +3568,10 @@ int sqp_waves(const ProblemDev& P, int batch) {
 }
 
 // segment-parallel Newton solves (SqpKernel::kSeg): the single-tile models on two or four waves per
-// instance, when the option allows it (P.seg) and each segment has at least two stages
+// instance, when the option allows it (P.seg) and the horizon has at least four stages (segments of one
+// stage or more).  (One wave running both segments' recursions interleaved was built and measured in
+// round 6 and does not pay: tools/one_wave_segments.patch)
+template <int ID>
 static bool sqp_seg_of(const ProblemDev& P, int nw) { return P.seg != 0 && nw >= 2 && P.H >= 4; }
 
 template <int ID>
@@ -3486,11 +3581,15 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
         // stage vectors split over two lanes when the H + 1 stages fit in half a wavefront
         const bool spl = P.H + 1 <= 32;
         const int nw = sqp_waves<ID>(P, batch);   // from the whole batch, also for a chunk of it
-        const bool seg = sqp_seg_of(P, nw);
+        const bool seg = sqp_seg_of<ID>(P, nw);
         if (nw == 4) {
-            if (seg)
-                return spl ? launch_sqp_variant<ID, 4, true, true>(P, S, io, batch, stream, first, count)
-                           : launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
+            if (seg) {
+                if constexpr (SqpKernel<ID, 4, true>::WSPL)   // the IPM split over the waves (lane = stage)
+                    return launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
+                else
+                    return spl ? launch_sqp_variant<ID, 4, true, true>(P, S, io, batch, stream, first, count)
+                               : launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
+            }
             return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream, first, count)
                        : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream, first, count);
         }
@@ -3521,7 +3620,7 @@ static bool overlap_ok_of(const ProblemDev& P, int batch) {
     const int nw = sqp_waves<ID>(P, batch);
     size_t lds = SqpKernel<ID>::lds_doubles(P.H);
     if constexpr (kDefaultWaves<ID> == 1) {
-        const bool seg = sqp_seg_of(P, nw);
+        const bool seg = sqp_seg_of<ID>(P, nw);
         if (nw == 4) lds = seg ? SqpKernel<ID, 4, true>::lds_doubles(P.H) : SqpKernel<ID, 4>::lds_doubles(P.H);
         if (nw == 2) lds = seg ? SqpKernel<ID, 2, true>::lds_doubles(P.H) : SqpKernel<ID, 2>::lds_doubles(P.H);
     }
@@ -3548,7 +3647,7 @@ template <int ID>
 static int segments_of(const ProblemDev& P, int batch) {
     if constexpr (kDefaultWaves<ID> == 1) {
         const int nw = sqp_waves<ID>(P, batch);
-        if (!sqp_seg_of(P, nw)) return 1;
+        if (!sqp_seg_of<ID>(P, nw)) return 1;
         return nw == 4 ? SqpKernel<ID, 4, true>::NSEG : SqpKernel<ID, 2, true>::NSEG;
     }
     return 1;

@@ -222,7 +222,8 @@ gpmpc_status gpmpc_get_launch_segments(gpmpc_handle* h, int32_t batch, int32_t* 
  *   GPMPC_TUNE_SEG         1 (default): segment-parallel Newton solves when a launch runs two or
  *                          four waves per instance (quad2d, cartpole): the horizon's two (two
  *                          waves) or three (four waves) segments are factorised and swept on
- *                          different waves at once and joined by a chain over the boundaries;
+ *                          different waves at once and joined by a chain over the boundaries
+ *                          (four waves: the IPM's elementwise work split over the waves too);
  *                          0: one wave runs the whole recursion; identical up to rounding */
 enum {
     GPMPC_TUNE_LIN_CACHE = 0,
@@ -239,7 +240,8 @@ gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value);
  * W = blkdiag(Q, R) scaled by dt on stages 0..H-1 and W_e = Q unscaled on stage H
  * (gpmpc/gpmpc.py:231-239, gpmpc/mpc.py:101-102, acados cost_scaling), y_k = [x_k; u_k],
  * y_ref,k = [reference window; u_eq].  Their sum is the objective value acados reports ("cost").
- * A failed solve (status 1 or 4) writes NaN.  NULL disables (default). */
+ * A solve that ends with any status other than 0 or 2 (a failed solve: its x, u hold the previous
+ * solution) writes NaN.  NULL disables (default). */
 gpmpc_status gpmpc_set_cost_buffer(gpmpc_handle* h, void* cost_dev);
 
 /* Kernel timing with HIP events recorded on the solve stream around the variance kernel

@@ -80,7 +80,7 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
                                                ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
 def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, seg):
     """seg = 1: the segment-parallel Newton solve (gpmpc_set_tuning GPMPC_TUNE_SEG): two segments on
-    two waves, three on four."""
+    two waves, three on four (there with the IPM's elementwise work split over the waves)."""
     # quad2d N=200 H=30: one of the 12 instances needs more than 25 SQP iterations for KKT 1e-9 at
     # step 1 (Gauss-Newton's linear rate; the C++ restatement stops there too)
     _run_against_cpp(name, N, H, B, steps, waves, all_converge=not (name == "quad2d" and H == 30), seg=seg)
@@ -122,7 +122,7 @@ def test_launch_segments_follow_waves_and_tuning():
 
     spec, _, _ = problem("quad2d", 20)
     gs = BatchSolver(spec, 30, 2)
-    for waves, seg, want in ((4, 1, 3), (2, 1, 2), (1, 1, 1), (4, 0, 1), (2, 0, 1)):
+    for waves, seg, want in ((4, 1, 3), (2, 1, 2), (1, 1, 1), (4, 0, 1), (2, 0, 1), (1, 0, 1)):
         gs.set_launch(waves=waves)
         gs.set_tuning(seg=seg)
         info = gs.launch_info()

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Round-4 A/B: one-wave SQP launches as four instances per workgroup (GPMPC_MI4) x overlapped
 # halves (GPMPC_OVERLAP), configs 3 / 4 / 5.  bash tools/ab_mi4.sh OUTDIR
 O=${1:?outdir}

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Round-4 A/B: (a) every launch ranked by cost (GPMPC_ORDER=2: the dispatcher then deals each cost
 # quartile across the CUs) vs instance order for launches the device holds at once (configs 3, 4);
 # (b) overlapped halves on/off for the multi-round config 5.  bash tools/ab_order.sh OUTDIR

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Round-4 A/B: overlapped step (cost-ranked halves, the second half's variance + SQP launches on a
 # side stream) vs one variance launch then one SQP launch (GPMPC_OVERLAP=0), configs 3 / 4 / 5.
 # bash tools/ab_overlap.sh OUTDIR

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Round-4 A/B: tightening variance with the column tiles split over 2 / 4 waves (gp_var_split_kernel,
 # the automatic choice at few points) vs one wave per point tile (GPMPC_VAR_SPLIT=1).  Run on the build
 # that still had the two-wave variant (GPMPC_VAR_SPLIT=2); the product keeps 1 and 4.

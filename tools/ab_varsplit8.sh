@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Round-4 A/B: tightening variance split over 4 vs 8 waves per point tile (GPMPC_VAR_SPLIT=4/8) vs one
 # (1) at the small shards, on the build that had the eight-wave variant (the product keeps 1 and 4).
 # bash tools/ab_varsplit8.sh OUTDIR

@@ -1,4 +1,6 @@
 #!/bin/bash
+# HISTORICAL (round 3/4): the library reads no environment variables since round 5, so the GPMPC_* settings
+# below no longer take effect; rerun with bench.py --lin-cache / --order / --overlap / --var-split / --waves.
 # Two waves per instance for batches of CUs < B <= 2 CUs (round 3): launch-shape parity, then the
 # config-3 shard of 512 instances and config 2 at B = 512 with waves auto (2) / 1 / 4.
 set -e

@@ -7,8 +7,8 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 make -C oracle asan
-log=profiles/r5/asan_cpu_ref.log
-mkdir -p profiles/r5
+log=${ASAN_LOG:-profiles/r6/asan_cpu_ref.log}
+mkdir -p "$(dirname "$log")"
 {
   echo "# $(date -u +%FT%TZ)  $(g++ --version | head -1)"
   echo "# build: make -C oracle asan (-fsanitize=address,undefined -fno-sanitize-recover=undefined -O1 -g)"
@@ -20,9 +20,14 @@ print('# loaded:', sorted({l.split()[-1] for l in open('/proc/self/maps') if 'as
   ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1 \
   UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
   OMP_NUM_THREADS=4 \
-    python -m pytest -p no:cacheprovider -q -m "not gpu" tests/test_cpu_ref.py tests/test_semantics_cpu.py 2>&1
-  echo "# exit status: $?"
+    python -m pytest -p no:cacheprovider -q -m "not gpu" tests/test_cpu_ref.py tests/test_semantics_cpu.py 2>&1 \
+    && rc=0 || rc=$?
+  echo "# pytest exit status: $rc"
+  echo "$rc" > "$log.rc"
 } > "$log" 2>&1 || true
 tail -5 "$log"
+rc=$(cat "$log.rc" 2>/dev/null || echo 1)
+rm -f "$log.rc"
 if grep -qE "ERROR: AddressSanitizer|runtime error:" "$log"; then echo "sanitizer reports found"; exit 1; fi
-echo "no sanitizer reports"
+if [ "$rc" != 0 ]; then echo "the tests failed under the sanitizers (pytest exit $rc)"; exit 1; fi
+echo "no sanitizer reports, tests passed"
