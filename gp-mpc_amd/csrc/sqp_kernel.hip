@@ -27,8 +27,8 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
-#ifndef GPMPC_WSPL_SEG   // (round-6 A/B of kWsplSeg: tools/build_variant.sh with -DGPMPC_WSPL_SEG=0)
-#define GPMPC_WSPL_SEG 1
+#ifndef GPMPC_PHASE_LANE   // (round-6 A/B of phase_lane: 0 off, 1 one-wave and quad3d kernels, 2 every kernel)
+#define GPMPC_PHASE_LANE 1
 #endif
 
 namespace gpmpc {
@@ -1470,7 +1470,8 @@ struct SqpKernel {
     // SQP loop, held across the IPM and spilled to AGPRs / scratch (reloaded with a memory latency per
     // phase).  Round 6: the quad2d / cartpole kernels' scratch 112-208 B/lane -> 0.
     __device__ static int phase_lane(int lane) {
-        asm volatile("" : "+v"(lane));
+        if constexpr (GPMPC_PHASE_LANE == 2 || (GPMPC_PHASE_LANE == 1 && (NWAVES == 1 || !kMfma)))
+            asm volatile("" : "+v"(lane));
         return lane;
     }
     // P_x,lambda of stage k of a lambda segment (in its P' block)
@@ -2413,14 +2414,6 @@ struct SqpKernel {
         constexpr int sg0 = seg_of_wave(0);
         return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd);
     }
-    // kWsplSeg: every wave is inside qp_ipm and runs its own part (the IPM's block barrier before the call
-    // stands for B1)
-    __device__ static bool seg_all(const Lds& L, int H, int lane, int w, int cmd) {
-        const int sg = seg_of_wave(w);
-        if (sg == NSEG - 1) return seg_part<2>(L, H, lane, w, sg, w == 1, cmd);
-        if (sg >= 0) return seg_part<1>(L, H, lane, w, sg, w == 1, cmd);
-        return seg_part<0>(L, H, lane, w, 0, false, cmd);
-    }
     // helper wave w's part of a segment command (after B1)
     __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
         const int sg = seg_of_wave(w);
@@ -2542,14 +2535,12 @@ struct SqpKernel {
     // NV variables' IPM state (the unsplit layout spilled 3.5 KB per lane to scratch at H = 40).  The
     // full step vector for the dynamics residual, the reductions and the Riccati status cross the
     // waves through LDS at block barriers; the Riccati recursion runs on wave 0.
-    // The single-tile models on four waves with the segment solve (round 6, kWsplSeg) split the same way:
-    // wave w holds variables 2w, 2w + 1 of every stage (NV = 2 against the two-lanes-per-stage split's 4
-    // on wave 0), and every wave calls the segment solve itself (seg_all) instead of wave 0 posting it.
-    // Without the segment solve, and on two waves (NV = 4 either way), they keep the SPL split on wave 0:
-    // there the helpers take the GP tile passes only (round 3 measured the cross-wave reductions costlier
-    // than the elementwise work they share at NB <= 8 while wave 0 also ran the whole recursion).
-    static constexpr bool kWsplSeg = GPMPC_WSPL_SEG && kSeg && NWAVES == 4;
-    static constexpr bool WSPL = NWAVES > 1 && (!kMfma || kWsplSeg);
+    // (the single-tile models keep their two-lanes-per-stage split on wave 0 when they run four waves:
+    // their helpers take the GP tile passes and the segment solves -- sharing the IPM's elementwise work
+    // costs more in cross-wave reductions than it saves at NB <= 8, round 3; with the segment solve, where
+    // every wave then runs its part of the solve from inside the IPM, the kernel spilled 400 B/lane and
+    // the 8-GPU shard's SQP kernel took 0.544 instead of 0.366 ms, round 6: tools/wspl_seg.patch)
+    static constexpr bool WSPL = NWAVES > 1 && !kMfma;
     // (WSPL: NWAVES NV may exceed NB -- cartpole's 5 variables in slots of 2 -- and the slots past NB
     // are inactive: never stored, never published)
     template <bool SPL>
@@ -2760,10 +2751,8 @@ struct SqpKernel {
                 TPHASE(4);
                 double dd[NV], dp[NX];
                 if constexpr (kSeg) {
-                    // segment-parallel solve: posted to the helper waves (seg_run), or every wave's own part (WSPL)
-                    bool rok;
-                    if constexpr (WSPL) rok = seg_all(L, H, lane, wv, kCmdSegFactor);
-                    else rok = seg_run(L, H, lane, kCmdSegFactor);
+                    // segment-parallel solve on the helper waves (seg_run)
+                    const bool rok = seg_run(L, H, lane, kCmdSegFactor);
                     if (!rok) { qp_ok = false; break; }
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
@@ -2844,8 +2833,7 @@ struct SqpKernel {
                 XSYNC();
                 TPHASE(5);
                 if constexpr (kSeg) {
-                    if constexpr (WSPL) (void)seg_all(L, H, lane, wv, kCmdSegVector);
-                    else (void)seg_run(L, H, lane, kCmdSegVector);
+                    (void)seg_run(L, H, lane, kCmdSegVector);
                     TPHASE(9);
                     recover_q<NV>(L, H, kq, vb, dd, dp);
                     TPHASE(3);
@@ -3583,13 +3571,9 @@ hipError_t launch_sqp_step(const ProblemDev& P, const StateDev& S, const StepIO&
         const int nw = sqp_waves<ID>(P, batch);   // from the whole batch, also for a chunk of it
         const bool seg = sqp_seg_of<ID>(P, nw);
         if (nw == 4) {
-            if (seg) {
-                if constexpr (SqpKernel<ID, 4, true>::WSPL)   // the IPM split over the waves (lane = stage)
-                    return launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
-                else
-                    return spl ? launch_sqp_variant<ID, 4, true, true>(P, S, io, batch, stream, first, count)
-                               : launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
-            }
+            if (seg)
+                return spl ? launch_sqp_variant<ID, 4, true, true>(P, S, io, batch, stream, first, count)
+                           : launch_sqp_variant<ID, 4, false, true>(P, S, io, batch, stream, first, count);
             return spl ? launch_sqp_variant<ID, 4, true>(P, S, io, batch, stream, first, count)
                        : launch_sqp_variant<ID, 4, false>(P, S, io, batch, stream, first, count);
         }

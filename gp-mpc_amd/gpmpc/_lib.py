@@ -88,10 +88,10 @@ def build_id() -> str:
 def build_info() -> dict:
     """The loaded library's build id, the tree's source hash and whether they match."""
     bid = build_id()
-    fields = dict(kv.split("=", 1) for kv in bid.split())
+    src = bid.split()[0][4:] if bid.startswith("src=") else None
     tree = source_hash()
-    return {"build_id": bid, "lib": str(LIB_PATH), "src_hash_lib": fields.get("src"), "src_hash_tree": tree,
-            "matches_tree": fields.get("src") == tree}
+    return {"build_id": bid, "lib": str(LIB_PATH), "src_hash_lib": src, "src_hash_tree": tree,
+            "matches_tree": src == tree}
 
 
 def load(require_gpu: bool = True):
