@@ -1988,10 +1988,11 @@ struct SqpKernel {
     // data for the corrector.
     // M is positive definite only while Ph is: a state direction that no cost, bound barrier or
     // coupling reaches (q_i = 0 on an unbounded or barely bounded state) leaves Ph singular and a
-    // pivot at rounding level.  Every pivot is checked against the largest diagonal entry of M
-    // (kPivRel): the return value false sends the solve to the one-segment recursion (seg_part's
-    // fallback), which never inverts Ph.
-    static constexpr double kPivRel = 1e-12;
+    // pivot at rounding level.  Every pivot is checked against the largest diagonal entry of Ph
+    // (kPivRel; M = Ph (I + W Ph) with W >= 0 has no smaller diagonal, and Ph is in every lane's
+    // registers already, so the check adds no cross-lane move to the chain): the return value false
+    // sends the solve to the one-segment recursion (seg_part's fallback), which never inverts Ph.
+    static constexpr double kPivRel = 1e-10;
     __device__ static bool seg_chain_full(const Lds& L, int H, int lane) {
         lane = phase_lane(lane);
         constexpr int CI = NX;
@@ -2035,15 +2036,16 @@ struct SqpKernel {
                 for (int l = 0; l < NX; ++l) acc = fma(pk[i <= l ? pidx(i, l) : pidx(l, i)], bv[l], acc);
                 col[i] = acc;
             }
-            double dmx = 0.0;   // largest diagonal entry of M (lane i holds column i)
+            double dmx = 0.0;   // largest diagonal entry of Ph
 #pragma unroll
-            for (int i = 0; i < NX; ++i) dmx = fmax(dmx, readlane_d(col[i], i));
+            for (int i = 0; i < NX; ++i) dmx = fmax(dmx, pk[pidx(i, i)]);
+            const double pmin = kPivRel * dmx;
 #pragma unroll
             for (int p = 0; p < NX; ++p) {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
-                piv_ok = piv_ok && (cp[p] > kPivRel * dmx);   // (false for a NaN pivot too)
+                piv_ok = piv_ok && (cp[p] > pmin);   // (false for a NaN pivot too)
                 const double inv = fast_rcp(cp[p]);
                 col[p] *= inv;
 #pragma unroll
