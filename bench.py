@@ -243,6 +243,9 @@ def parse_args(argv=None):
                     help="cost-ordered dispatch (gpmpc_set_tuning GPMPC_TUNE_ORDER; default: the library's)")
     ap.add_argument("--var-split", type=int, choices=[0, 1, 4], default=None,
                     help="triangular variance kernel's column split (gpmpc_set_tuning GPMPC_TUNE_VAR_SPLIT)")
+    ap.add_argument("--tail", type=int, default=None,
+                    help="tail boost: the K costliest instances of a one-wave, one-round step as two-wave segment "
+                         "solves on a high-priority stream (gpmpc_set_tuning GPMPC_TUNE_TAIL; default: the library's)")
     ap.add_argument("--waves", type=int, choices=[0, 1, 2, 4], default=None,
                     help="SQP-kernel waves per instance (gpmpc_set_launch; default 0 = automatic)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",
@@ -416,7 +419,7 @@ def run_gpu(args, rank, local_rank, world, weak_secondary=False):
             solver.set_tuning(seg=args.seg)
         if args.overlap is not None:
             solver.set_tuning(overlap=args.overlap)
-        for opt in ("lin_cache", "order", "var_split"):
+        for opt in ("lin_cache", "order", "var_split", "tail"):
             if getattr(args, opt) is not None:
                 solver.set_tuning(**{opt: getattr(args, opt)})
         if args.waves is not None:

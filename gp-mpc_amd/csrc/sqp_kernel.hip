@@ -27,6 +27,13 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
+#ifndef GPMPC_SEG_FALLBACK   // 1: boundary-chain pivot check and one-segment fallback (A/B variants: 0 neither,
+                             // 2 the check and its flag without the fallback, 3 the fallback without the check)
+#define GPMPC_SEG_FALLBACK 1
+#endif
+#ifndef GPMPC_SOLVE_STAMP    // 1: per-instance solve time in stats slots 10-11 (A/B variants: 0)
+#define GPMPC_SOLVE_STAMP 1
+#endif
 #ifndef GPMPC_PHASE_LANE   // (round-6 A/B of phase_lane: 0 off, 1 one-wave and quad3d kernels, 2 every kernel)
 #define GPMPC_PHASE_LANE 1
 #endif
@@ -2045,7 +2052,7 @@ struct SqpKernel {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
-                piv_ok = piv_ok && (cp[p] > pmin);   // (false for a NaN pivot too)
+                piv_ok = piv_ok && (GPMPC_SEG_FALLBACK == 3 || cp[p] > pmin);   // (false for a NaN pivot too)
                 const double inv = fast_rcp(cp[p]);
                 col[p] *= inv;
 #pragma unroll
@@ -2307,10 +2314,14 @@ struct SqpKernel {
     //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain, others: affine columns |
     //                 Bm2 | forward | B2
     // Factorisation statuses in ctrl[8 + w].  Fallback: when the boundary chain meets a pivot it cannot
-    // trust (seg_chain_full), it sets ctrl[kFb]; after Bm2 the chain wave then runs the one-segment
-    // recursion over the whole horizon in the same layout (factorisation into ctrl[kFb + 1], closed-loop
-    // maps, forward sweep from dx_0 = 0) before B2, and the corrector of the same IPM iteration runs its
-    // one-segment vector pass, maps and sweep between B1 and Bm1.  Same barriers on every wave.
+    // trust (seg_chain_full), it sets ctrl[kFb]; every wave reads the flag after Bm2 but the segments'
+    // fold and sweep run regardless, and after B2 the chain wave runs the one-segment recursion over the
+    // whole horizon in the same layout (factorisation into ctrl[kFb + 1], closed-loop maps, forward
+    // sweep from dx_0 = 0), overwriting what they wrote, before an extra barrier B3; the corrector of
+    // the same IPM iteration likewise runs its one-segment vector pass, maps and sweep after its B2.
+    // Same barriers on every wave (the flag is the workgroup's).  Reading the flag only where the
+    // common path does not wait on it keeps the fallback's cost off that path (a flag tested before
+    // the sweeps cost the 4- and 8-GPU shards 3 %, profiles/r6/ab_fallback/).
     static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
     static constexpr int kFb = 12;   // ctrl slots: fallback flag, fallback factorisation status
     static constexpr int kTs = 14;   // ctrl slots 14-15: the instance's start time stamp (stats slot 10)
@@ -2355,12 +2366,17 @@ struct SqpKernel {
             }
             if (chain && ok) {
                 const bool cok = seg_chain_full(L, H, lane);
-                if (lane == 0) L.ctrl[kFb] = cok ? 0 : 1;
+                if constexpr (GPMPC_SEG_FALLBACK) {
+                    if (lane == 0) L.ctrl[kFb] = cok ? 0 : 1;
+                }
             }
             if (a1 > a0) seg_acl<true>(L, lane, a0, a1);
             __syncthreads();   // Bm2: lambda_b, x_w, A'_k
-            const bool fb = ok && L.ctrl[kFb] != 0;
-            if (ok && !fb) {
+            // (the fallback flag is read here and used after B2: the segments' fold and sweep run
+            // whatever it says, and a fallback overwrites what they wrote, so the common path never
+            // waits on the flag's LDS round trip)
+            const int fbf = GPMPC_SEG_FALLBACK != 0 ? L.ctrl[kFb] : 0;
+            if (ok) {
                 if constexpr (KIND == 1) {
                     seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
                     WSYNC();
@@ -2369,43 +2385,48 @@ struct SqpKernel {
                     seg_forward(L, lane, k0, H, xs, true);
                 }
             }
-            if (fb && chain) {   // the one-segment recursion instead (Ph singular at a boundary)
-                const bool fok = seg_factor<false>(L, H, lane, 0, H, nullptr);
-                if (lane == 0) L.ctrl[kFb + 1] = fok ? 1 : 0;
+            __syncthreads();   // B2
+            if ((GPMPC_SEG_FALLBACK & 1) && ok && fbf != 0) {   // (uniform over the workgroup: every wave read the flag)
+                if (chain) {   // the one-segment recursion instead (Ph singular at a boundary)
+                    const bool fok = seg_factor<false>(L, H, lane, 0, H, nullptr);
+                    if (lane == 0) L.ctrl[kFb + 1] = fok ? 1 : 0;
+                    WSYNC();
+                    if (fok) {
+                        seg_acl<true>(L, lane, 0, H);
+                        WSYNC();
+                        seg_forward(L, lane, 0, H, nullptr, true);
+                    }
+                }
+                __syncthreads();   // B3 (fallback only)
+                ok = L.ctrl[kFb + 1] != 0;
+            }
+        } else {
+            // (this IPM iteration's predictor set the flag; as there, the segments' passes run whatever
+            // it says and a fallback overwrites their results after B2)
+            const int fbf = GPMPC_SEG_FALLBACK != 0 ? L.ctrl[kFb] : 0;
+            if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
+            if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
+            __syncthreads();   // Bm1
+            if (chain) seg_chain_vec(L, H, lane);
+            if (a1 > a0) seg_acl<false>(L, lane, a0, a1);
+            __syncthreads();   // Bm2: lambda_b, x_w, A'_k[:, CI]
+            if constexpr (KIND == 1) {
+                seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
                 WSYNC();
-                if (fok) {
-                    seg_acl<true>(L, lane, 0, H);
+                seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
+            } else if constexpr (KIND == 2) {
+                seg_forward(L, lane, k0, H, xs, true);
+            }
+            __syncthreads();   // B2
+            if ((GPMPC_SEG_FALLBACK & 1) && fbf != 0) {
+                if (chain) {
+                    seg_vector_backward(L, H, lane, 0, H, true, nullptr);
+                    seg_acl<false>(L, lane, 0, H);
                     WSYNC();
                     seg_forward(L, lane, 0, H, nullptr, true);
                 }
+                __syncthreads();   // B3 (fallback only)
             }
-            __syncthreads();   // B2
-            if (fb) ok = L.ctrl[kFb + 1] != 0;
-        } else {
-            const bool fb = L.ctrl[kFb] != 0;   // (this IPM iteration's predictor)
-            if (!fb) {
-                if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
-                if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
-            } else if (chain) {
-                seg_vector_backward(L, H, lane, 0, H, true, nullptr);
-                seg_acl<false>(L, lane, 0, H);
-                WSYNC();
-                seg_forward(L, lane, 0, H, nullptr, true);
-            }
-            __syncthreads();   // Bm1
-            if (chain && !fb) seg_chain_vec(L, H, lane);
-            if (a1 > a0 && !fb) seg_acl<false>(L, lane, a0, a1);
-            __syncthreads();   // Bm2: lambda_b, x_w, A'_k[:, CI]
-            if (!fb) {
-                if constexpr (KIND == 1) {
-                    seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
-                    WSYNC();
-                    seg_forward(L, lane, k0, k1, sg ? xs : nullptr, false);
-                } else if constexpr (KIND == 2) {
-                    seg_forward(L, lane, k0, H, xs, true);
-                }
-            }
-            __syncthreads();   // B2
         }
         return ok;
     }
@@ -3042,7 +3063,9 @@ struct SqpKernel {
         // instance solve time (stats slots 10-11), stamped once the instance state is loaded: the stamp
         // waits in an LDS slot (taken at the kernel's first instruction, or held in registers, it cost the
         // one-wave kernel 48 B/lane of scratch)
-        if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(L.ctrl + kTs) = __builtin_amdgcn_s_memrealtime();
+        if constexpr (GPMPC_SOLVE_STAMP) {
+            if (threadIdx.x == 0) *reinterpret_cast<unsigned long long*>(L.ctrl + kTs) = __builtin_amdgcn_s_memrealtime();
+        }
 
         TPHASE(0);
         // ---------------- constraint tightening from the previous solution (gpmpc.py:425-498)
@@ -3390,10 +3413,12 @@ struct SqpKernel {
                 st[7] = max(st[7], (long long)it);
                 st[8] = max(st[8], (long long)qp_total);
                 st[9] += x0_ok ? it + 1 - (lin_hit ? 1 : 0) : 0;   // linearisations computed
-                const long long dt = (long long)(__builtin_amdgcn_s_memrealtime() -
-                                                 *reinterpret_cast<const unsigned long long*>(L.ctrl + kTs));   // 100 MHz ticks
-                st[10] += dt;
-                st[11] = dt;
+                if constexpr (GPMPC_SOLVE_STAMP) {
+                    const long long dt = (long long)(__builtin_amdgcn_s_memrealtime() -
+                                                     *reinterpret_cast<const unsigned long long*>(L.ctrl + kTs));   // 100 MHz ticks
+                    st[10] += dt;
+                    st[11] = dt;
+                }
             }
         }
     }
