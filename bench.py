@@ -245,7 +245,8 @@ def parse_args(argv=None):
                     help="triangular variance kernel's column split (gpmpc_set_tuning GPMPC_TUNE_VAR_SPLIT)")
     ap.add_argument("--tail", type=int, default=None,
                     help="tail boost: the K costliest instances of a one-wave, one-round step as two-wave segment "
-                         "solves on a high-priority stream (gpmpc_set_tuning GPMPC_TUNE_TAIL; default: the library's)")
+                         "solves beside the others' one-wave launch (gpmpc_set_tuning GPMPC_TUNE_TAIL: -1 as many as "
+                         "the launch leaves SIMDs free, 0 off; default: the library's, -1)")
     ap.add_argument("--waves", type=int, choices=[0, 1, 2, 4], default=None,
                     help="SQP-kernel waves per instance (gpmpc_set_launch; default 0 = automatic)")
     ap.add_argument("--var-inputs", choices=["reference", "dynamics"], default="reference",

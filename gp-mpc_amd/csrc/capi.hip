@@ -117,6 +117,10 @@ struct gpmpc_handle {
     double* stage_cost = nullptr;   // caller's [max_batch][H+1] stage-cost buffer (StepIO::stage_cost)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // tail boost (GPMPC_TUNE_TAIL): the costliest `tail` instances of a one-wave, one-round step run
+    // as two-wave segment solves on the caller's stream, the others' one-wave launch on `side`
+    // (-1: as many as the launch leaves SIMDs free, sqp_tail_spare)
+    int tail = -1;
 };
 
 // The handle's device state (iterate, multipliers, variances, dispatch order) is read and written
@@ -150,6 +154,35 @@ struct StreamMark {
         h->last_stream = s;
     }
 };
+
+// The second stream of overlapped and tail-boosted steps and its fork / join events (lowest
+// priority), created together on first use or not at all.
+static hipError_t ensure_side(gpmpc_handle* h) {
+    if (h->side) return hipSuccess;
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipError_t ce = hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo);   // lowest priority
+    if (ce == hipSuccess) ce = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    if (ce == hipSuccess) ce = hipEventCreateWithFlags(&join, hipEventDisableTiming);
+    if (ce != hipSuccess) {
+        if (join) (void)hipEventDestroy(join);
+        if (fork) (void)hipEventDestroy(fork);
+        if (side) (void)hipStreamDestroy(side);
+        return ce;
+    }
+    h->side = side;
+    h->ev_fork = fork;
+    h->ev_join = join;
+    return hipSuccess;
+}
+
+// Instances the tail boost runs on two waves for this step (0: none, the ordinary launch)
+static int tail_count(const gpmpc_handle* h, const ProblemDev& P, int batch) {
+    if (h->tail == 0 || !sqp_tail_ok(P, batch)) return 0;
+    return h->tail < 0 ? sqp_tail_spare(P, batch) : std::min(h->tail, batch - 1);
+}
 
 static hipEvent_t take_event(gpmpc_handle* h) {
     while (!h->ev_pool.empty()) {
@@ -678,24 +711,8 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
     // the solves that set its length begin.  Each instance's arithmetic is unchanged (same kernels,
     // same per-instance data), so the results are bit-identical to the sequential order.
     if (var_launch && h->overlap && batch >= 2 && batch <= 16384 && sqp_overlap_ok(P, batch)) {
-        if (!h->side) {   // created together or not at all
-            int lo = 0, hi = 0;
-            if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
-            hipStream_t side = nullptr;
-            hipEvent_t fork = nullptr, join = nullptr;
-            hipError_t ce = hipStreamCreateWithPriority(&side, hipStreamNonBlocking, lo);   // lowest priority
-            if (ce == hipSuccess) ce = hipEventCreateWithFlags(&fork, hipEventDisableTiming);
-            if (ce == hipSuccess) ce = hipEventCreateWithFlags(&join, hipEventDisableTiming);
-            if (ce != hipSuccess) {
-                if (join) (void)hipEventDestroy(join);
-                if (fork) (void)hipEventDestroy(fork);
-                if (side) (void)hipStreamDestroy(side);
-                return fail(GPMPC_ERR_HIP, std::string("side stream: ") + hipGetErrorString(ce));
-            }
-            h->side = side;
-            h->ev_fork = fork;
-            h->ev_join = join;
-        }
+        if (const hipError_t ce = ensure_side(h); ce != hipSuccess)
+            return fail(GPMPC_ERR_HIP, std::string("side stream: ") + hipGetErrorString(ce));
         const int b1 = (batch + 1) / 2, b2 = batch - b1;
         HIPCHK(launch_sqp_order(S, batch, s));
         if (h->profiling) {
@@ -790,8 +807,41 @@ gpmpc_status gpmpc_solve(gpmpc_handle* h, int32_t batch, const double* x0, const
         else if (e0) h->ev_pool.push_back(e0);
         if (e1) h->ev_pool.push_back(e1);
     };
-    const hipError_t le = launch_sqp(P, S, io, batch, s);
+    // Tail boost (GPMPC_TUNE_TAIL = K > 0): a launch that gives every instance one wave in one round
+    // of workgroups (the metric's 1024 quad2d instances on one MI355X) lasts as long as its slowest
+    // instance, and the costliest instances stay costly from step to step (StateDev::cost).  The
+    // instances are ranked by the cost of their previous solve; the K costliest run as two-wave
+    // segment solves (their recursions split over two waves) on the caller's stream, right behind the
+    // ranking kernel, and the others as one-wave instances on the side stream, released by the same
+    // ranking kernel (the side stream's wait resolves after the caller's next packet is dispatched, so
+    // the two-wave instances take their SIMDs first).  With one SIMD per wave the K extra waves make
+    // the K cheapest instances (dispatched last) wait for the SIMDs of the first instances to finish.
+    // Each instance's arithmetic is its launch shape's, identical up to rounding to the one-wave
+    // solve (the parity tests cover both shapes).
+    bool tail_queued = false;
+    auto launch_step = [&]() -> hipError_t {
+        const int K = tail_count(h, P, batch);
+        if (K <= 0) return launch_sqp(P, S, io, batch, s);
+        hipError_t e = ensure_side(h);
+        if (e == hipSuccess) e = launch_sqp_order(S, batch, s);
+        if (e == hipSuccess) e = hipEventRecord(h->ev_fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(h->side, h->ev_fork, 0);
+        if (e != hipSuccess) return e;
+        ProblemDev P2 = P, P1 = P;
+        P2.waves = 2;   // (sqp_tail_ok: segment solves on two waves)
+        P1.waves = 1;
+        e = launch_sqp(P2, S, io, batch, s, 0, K);
+        if (e == hipSuccess) tail_queued = true;
+        if (e == hipSuccess) e = launch_sqp(P1, S, io, batch, h->side, K, batch - K);
+        // the join is recorded whatever happened above, so the caller's stream never runs ahead of
+        // work already queued on the side stream
+        const hipError_t je = hipEventRecord(h->ev_join, h->side);
+        const hipError_t we = je == hipSuccess ? hipStreamWaitEvent(s, h->ev_join, 0) : je;
+        return e == hipSuccess ? we : e;
+    };
+    const hipError_t le = launch_step();
     if (le != hipSuccess) {
+        if (tail_queued) h->any_prev = true;   // part of the batch's iterate is being updated
         recycle();
         return fail(GPMPC_ERR_HIP, std::string("launch_sqp: ") + hipGetErrorString(le));
     }
@@ -834,9 +884,11 @@ gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* wave
     if (batch < 1 || batch > h->max_batch) return fail(GPMPC_ERR_ARG, "batch out of range");
     if (waves) *waves = sqp_launch_waves(h->P, batch);
     // the overlap needs a variance launch (tightening with GPs) besides the shape
-    if (overlapped)
+    if (overlapped) {
         *overlapped = (h->overlap && h->P.tighten && h->P.use_gp && batch >= 2 && batch <= 16384 &&
                        sqp_overlap_ok(h->P, batch)) ? 1 : 0;
+        if (*overlapped == 0 && tail_count(h, h->P, batch) > 0) *overlapped = 2;   // tail boost
+    }
     return GPMPC_OK;
 }
 
@@ -871,6 +923,10 @@ gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value) {
         case GPMPC_TUNE_SEG:
             if (value != 0 && value != 1) break;
             h->P.seg = value;
+            return GPMPC_OK;
+        case GPMPC_TUNE_TAIL:
+            if (value < -1 || value > 16384) break;
+            h->tail = value;
             return GPMPC_OK;
         case GPMPC_TUNE_EVENT_FENCE:
             if (value != 0 && value != 1) break;

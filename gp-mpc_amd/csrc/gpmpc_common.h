@@ -245,6 +245,8 @@ hipError_t launch_sqp(const ProblemDev& P, const StateDev& S, const StepIO& io, 
                       int first = 0, int count = -1);
 hipError_t launch_sqp_order(const StateDev& S, int batch, hipStream_t stream);
 bool sqp_overlap_ok(const ProblemDev& P, int batch);
+bool sqp_tail_ok(const ProblemDev& P, int batch);   // GPMPC_TUNE_TAIL applies (gpmpc_solve)
+int sqp_tail_spare(const ProblemDev& P, int batch);  // its automatic K: SIMDs the one-wave launch leaves free
 int sqp_launch_waves(const ProblemDev& P, int batch);   // waves per instance launch_sqp would use
 int sqp_launch_segments(const ProblemDev& P, int batch);   // horizon segments of its Newton solves
 size_t sqp_lds_bytes(int model, int H);

@@ -3646,6 +3646,41 @@ bool sqp_overlap_ok(const ProblemDev& P, int batch) {
     }
     return false;
 }
+// Whether a step may run the tail boost (gpmpc_solve, GPMPC_TUNE_TAIL): a single-tile model whose
+// automatic launch gives every instance one wave in one round of workgroups, segment solves on.
+template <int ID>
+static bool tail_ok_of(const ProblemDev& P, int batch) {
+    if constexpr (kDefaultWaves<ID> == 1) {
+        return P.waves == 0 && P.n_cu > 0 && batch >= 2 && sqp_waves<ID>(P, batch) == 1 &&
+               sqp_seg_of<ID>(P, 2) && !overlap_ok_of<ID>(P, batch);
+    }
+    return false;
+}
+bool sqp_tail_ok(const ProblemDev& P, int batch) {
+    switch (P.model) {
+        case kQuad2D: return tail_ok_of<kQuad2D>(P, batch);
+        case kQuad3D: return tail_ok_of<kQuad3D>(P, batch);
+        case kCartpole: return tail_ok_of<kCartpole>(P, batch);
+    }
+    return false;
+}
+// The SIMDs a one-wave, one-round launch of `batch` instances leaves free (0 when the tail boost
+// does not apply): the automatic K of GPMPC_TUNE_TAIL, one extra wave per boosted instance.
+template <int ID>
+static int tail_spare_of(const ProblemDev& P, int batch) {
+    if (!tail_ok_of<ID>(P, batch)) return 0;
+    const size_t lds = SqpKernel<ID>::lds_doubles(P.H) * sizeof(double);
+    const int per_cu = std::max(1, std::min(4, (int)((160 * 1024) / lds)));
+    return std::max(0, std::min(P.n_cu * per_cu - batch, batch - 1));
+}
+int sqp_tail_spare(const ProblemDev& P, int batch) {
+    switch (P.model) {
+        case kQuad2D: return tail_spare_of<kQuad2D>(P, batch);
+        case kQuad3D: return tail_spare_of<kQuad3D>(P, batch);
+        case kCartpole: return tail_spare_of<kCartpole>(P, batch);
+    }
+    return 0;
+}
 int sqp_launch_waves(const ProblemDev& P, int batch) {
     switch (P.model) {
         case kQuad2D: return sqp_waves<kQuad2D>(P, batch);

@@ -210,11 +210,11 @@ class BatchSolver:
         w, o, g = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         _lib.check(self.lib.gpmpc_get_launch_info(self._h, self.batch, ctypes.byref(w), ctypes.byref(o)))
         _lib.check(self.lib.gpmpc_get_launch_segments(self._h, self.batch, ctypes.byref(g)))
-        return {"waves": w.value, "segments": g.value, "overlapped": bool(o.value)}
+        return {"waves": w.value, "segments": g.value, "overlapped": o.value == 1, "tail_boost": o.value == 2}
 
     def set_tuning(self, **opts):
         """Performance switches (gpmpc_set_tuning): lin_cache=0/1, order=0/1/2, overlap=0/1,
-        var_split=0/1/4, event_fence=0/1, seg=0/1.  Outputs do not depend on them (A/B knobs)."""
+        var_split=0/1/4, event_fence=0/1, seg=0/1, tail=K.  Outputs do not depend on them (A/B knobs)."""
         for k, v in opts.items():
             if k not in _lib.TUNE:
                 raise ValueError(f"unknown tuning option {k!r} (one of {sorted(_lib.TUNE)})")

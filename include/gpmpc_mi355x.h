@@ -198,7 +198,9 @@ gpmpc_status gpmpc_set_launch(gpmpc_handle* h, int32_t waves);
  * launch runs as two overlapped halves (see gpmpc_solve).  With overlapped = 1 the profiling
  * events of gpmpc_kernel_times bracket the costlier half's variance launch ("variance") and the
  * span from its end to the join of both halves' SQP launches ("SQP", which also contains the
- * cheaper half's variance launch): spans of the step, not per-kernel durations. */
+ * cheaper half's variance launch): spans of the step, not per-kernel durations.  overlapped = 2:
+ * the tail boost of GPMPC_TUNE_TAIL applies (two SQP launches side by side, the "SQP" events
+ * bracketing both; `waves` is then the other instances' one). */
 gpmpc_status gpmpc_get_launch_info(gpmpc_handle* h, int32_t batch, int32_t* waves, int32_t* overlapped);
 
 /* Horizon segments of the Newton solves gpmpc_solve would run for `batch` instances (host, no
@@ -222,16 +224,24 @@ gpmpc_status gpmpc_get_launch_segments(gpmpc_handle* h, int32_t batch, int32_t* 
  *   GPMPC_TUNE_SEG         1 (default): segment-parallel Newton solves when a launch runs two or
  *                          four waves per instance (quad2d, cartpole): the horizon's two (two
  *                          waves) or three (four waves) segments are factorised and swept on
- *                          different waves at once and joined by a chain over the boundaries
- *                          (four waves: the IPM's elementwise work split over the waves too);
- *                          0: one wave runs the whole recursion; identical up to rounding */
+ *                          different waves at once and joined by a chain over the boundaries;
+ *                          0: one wave runs the whole recursion; identical up to rounding
+ *   GPMPC_TUNE_TAIL        -1 (default): automatic, K = the SIMDs the launch leaves free (4 x CUs - B,
+ *                          so 0 at B = 4 x CUs); 0: off; K > 0: fixed.  A step whose SQP launch gives
+ *                          every instance one wave in one round of workgroups (quad2d, cartpole; batch
+ *                          between 2 and 4 x CUs, waves automatic, segments on) runs its K costliest
+ *                          instances (by the cost of their previous solve) as two-wave segment solves
+ *                          on the caller's stream, beside the other instances' one-wave launch on a
+ *                          second stream; identical up to rounding (each instance's arithmetic is that of
+ *                          its launch shape).  The SQP profiling events then bracket both launches */
 enum {
     GPMPC_TUNE_LIN_CACHE = 0,
     GPMPC_TUNE_ORDER = 1,
     GPMPC_TUNE_OVERLAP = 2,
     GPMPC_TUNE_VAR_SPLIT = 3,
     GPMPC_TUNE_EVENT_FENCE = 4,
-    GPMPC_TUNE_SEG = 5
+    GPMPC_TUNE_SEG = 5,
+    GPMPC_TUNE_TAIL = 6
 };
 gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value);
 

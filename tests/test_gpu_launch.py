@@ -80,7 +80,7 @@ def _run_against_cpp(name, N, H, B, steps, waves, all_converge=True, seg=0):
                                                ("quad2d", 120, 15, 6, 3), ("cartpole", 40, 10, 6, 3)])
 def test_launch_shapes_match_cpp_restatement(name, N, H, B, steps, waves, seg):
     """seg = 1: the segment-parallel Newton solve (gpmpc_set_tuning GPMPC_TUNE_SEG): two segments on
-    two waves, three on four (there with the IPM's elementwise work split over the waves)."""
+    two waves, three on four."""
     # quad2d N=200 H=30: one of the 12 instances needs more than 25 SQP iterations for KKT 1e-9 at
     # step 1 (Gauss-Newton's linear rate; the C++ restatement stops there too)
     _run_against_cpp(name, N, H, B, steps, waves, all_converge=not (name == "quad2d" and H == 30), seg=seg)
@@ -129,7 +129,7 @@ def test_launch_segments_follow_waves_and_tuning():
         assert info["waves"] == waves and info["segments"] == want, (waves, seg, info)
     gs.set_launch(waves=0)
     gs.set_tuning(seg=1)
-    assert gs.launch_info() == {"waves": 4, "segments": 3, "overlapped": False}   # 2 instances <= CUs
+    assert gs.launch_info() == {"waves": 4, "segments": 3, "overlapped": False, "tail_boost": False}   # 2 <= CUs
     q3 = BatchSolver(get_spec("quad3d"), 10, 2)
     assert q3.launch_info()["segments"] == 1
 
@@ -228,4 +228,52 @@ def _seg_vs_one_segment(spec, data, hyp, mats, H, waves):
         ex = np.abs(x_1 - x_0).max(axis=(1, 2)) / (1 + np.abs(x_0).max(axis=(1, 2)))
         eu = np.abs(u_1 - u_0).max(axis=(1, 2)) / (1 + np.abs(u_0).max(axis=(1, 2)))
         assert max(ex[ok].max(), eu[ok].max()) <= 1e-6, (s, ex[ok].max(), eu[ok].max())
+        x = solvers[0].plant_step(x, c0)
+
+
+def test_tail_boost_matches_one_wave_launch():
+    """GPMPC_TUNE_TAIL: with one wave per instance in one round of workgroups (2 CUs < B <= 4 CUs),
+    the K costliest instances of the previous solve run two-wave segment solves beside the others'
+    one-wave launch on a second stream -- by default (-1) as many as the launch leaves SIMDs free,
+    none at B = 4 CUs (the metric's single-GPU shape).  Same closed loop as tail = 0 at KKT 1e-9 for
+    the automatic K and a fixed K = 64: every instance converged on both sides agrees to 1e-6
+    (1 + |.|), the statuses agree but for at most B / 100 borderline instances at the SQP limit."""
+    torch = _torch()
+    from gpmpc.solver import BatchSolver
+
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    spec, data, hyp = problem("quad2d", 200)
+    mats = lqr(spec)
+    full = BatchSolver(spec, 30, 4 * n_cu)
+    assert full.launch_info()["tail_boost"] is False   # no SIMD left free: the ordinary launch
+    H, B, steps = 30, 2 * n_cu + 88, 4
+    solvers = []
+    for tail in (0, -1, 64):
+        gs = BatchSolver(spec, H, B, tol=1e-9, qp_tol=1e-11, qp_max_iter=100)
+        if tail >= 0:
+            gs.set_tuning(tail=tail)
+        gs.set_gps(product_gps(data, hyp))
+        gs.set_tightening(True, 0.95, *mats)
+        gs.reset(reset_iterate=True)
+        info = gs.launch_info()
+        assert info["waves"] == 1 and info["tail_boost"] == (tail != 0), info
+        solvers.append(gs)
+    x0, phase = initial_states(spec, spec.reference_trajectory(), B, seed=3)
+    x = torch.tensor(x0, device="cuda")
+    for s in range(steps):
+        ph = torch.tensor(phase + s, dtype=torch.int32, device="cuda")
+        outs = []
+        for gs in solvers:
+            u = gs.solve(x, ph).clone()
+            xs, us, _ = (t.cpu().numpy() for t in gs.solution())
+            outs.append((gs.status.cpu().numpy(), xs, us, u))
+        st0, x_0, u_0, c0 = outs[0]
+        for st1, x_1, u_1, _ in outs[1:]:
+            both = (st0 == 0) & (st1 == 0)
+            assert both.sum() >= B - max(1, B // 100), (s, np.bincount(st0, minlength=5), np.bincount(st1, minlength=5))
+            ex = np.abs(x_1 - x_0).max(axis=(1, 2)) / (1 + np.abs(x_0).max(axis=(1, 2)))
+            eu = np.abs(u_1 - u_0).max(axis=(1, 2)) / (1 + np.abs(u_0).max(axis=(1, 2)))
+            assert max(ex[both].max(), eu[both].max()) <= 1e-6, (s, ex[both].max(), eu[both].max())
+            diff = st0 != st1
+            assert diff.sum() <= max(1, B // 100) and set(st0[diff]) | set(st1[diff]) <= {0, 2}, (s, st0[diff], st1[diff])
         x = solvers[0].plant_step(x, c0)
