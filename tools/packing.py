@@ -8,8 +8,10 @@ order (the SQP / IPM iteration counts of that step, StateDev::cost).  For each s
 measured instance times greedily on `slots` CUs (a workgroup starts on the first CU to free up, in
 dispatch order), for three orders:
   ranked   - by the previous step's cost, what the kernel dispatched (GPMPC_TUNE_ORDER 1)
+  prevtime - by the previous step's measured solve times instead (a candidate predictor)
   ideal    - by this step's own times (longest first: what a perfect cost prediction would give)
   instance - instance order (GPMPC_TUNE_ORDER 0)
+  xcd      - the ranked order with each workgroup bound to XCD (dispatch index % 8), 32 CUs each
 and prints them beside the step's measured SQP-kernel time and the lower bound max(slowest instance,
 sum of times / slots).  The schedule ignores contention between CUs, so "ranked" against the measured
 time says how much of the kernel is packing and how much is the instances themselves.
@@ -29,14 +31,18 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gp-mpc_amd"))
 
 
-def makespan(times, order, slots):
-    free = [0.0] * slots
-    heapq.heapify(free)
+def makespan(times, order, slots, xcds=1):
+    """Greedy list schedule of `order` on `slots` CUs.  xcds > 1: the CUs split evenly over that many
+    XCDs and the workgroup of dispatch index r goes to XCD r % xcds (each XCD then schedules its own
+    subsequence on its own CUs), as the MI355X's command processor distributes workgroups."""
     end = 0.0
-    for b in order:
-        t = heapq.heappop(free) + times[b]
-        end = max(end, t)
-        heapq.heappush(free, t)
+    for x in range(xcds):
+        free = [0.0] * (slots // xcds)
+        heapq.heapify(free)
+        for b in list(order)[x::xcds]:
+            t = heapq.heappop(free) + times[b]
+            end = max(end, t)
+            heapq.heappush(free, t)
     return end
 
 
@@ -93,7 +99,7 @@ def main():
     slots = args.slots or torch.cuda.get_device_properties(0).multi_processor_count
     k_lin = 5 if spec.name == "quad3d" else 3   # SqpKernel::kCostLin (NB + 1 > 16 for quad3d)
     solver.set_profiling(True)
-    prev_cost = None
+    prev_cost = prev_times = None
     rows = []
     for s in range(args.warmup + args.steps):
         before = stats[:, :2].clone()
@@ -107,16 +113,21 @@ def main():
         if s >= args.warmup and prev_cost is not None:
             ranked = np.lexsort((np.arange(B), -prev_cost))   # order_by_cost_kernel: cost desc, index asc
             ideal = np.argsort(-times, kind="stable")
+            prevt = np.argsort(-prev_times, kind="stable")
             rows.append({"step": s, "kernel_ms": sqp_ms[-1] if sqp_ms else None,
-                         "ranked_ms": makespan(times, ranked, slots), "ideal_ms": makespan(times, ideal, slots),
+                         "ranked_ms": makespan(times, ranked, slots), "prevtime_ms": makespan(times, prevt, slots),
+                         "ideal_ms": makespan(times, ideal, slots),
                          "instance_ms": makespan(times, np.arange(B), slots),
+                         "xcd_ms": makespan(times, ranked, slots, 8),
                          "bound_ms": max(times.max(), times.sum() / slots), "slowest_ms": float(times.max()),
                          "mean_ms": float(times.mean())})
-        prev_cost = cost.astype(np.float64)
-    print("step  kernel  ranked  ideal  instance  bound  slowest  mean   (ms; schedules of the measured instance times)")
+        prev_cost, prev_times = cost.astype(np.float64), times.copy()
+    print("step  kernel  ranked  prevtime  ideal  instance  xcd  bound  slowest  mean   (ms; schedules of the "
+          "measured instance times)")
     for r in rows:
-        print(f"{r['step']:4d}  {r['kernel_ms'] or float('nan'):6.3f}  {r['ranked_ms']:6.3f}  {r['ideal_ms']:5.3f}  "
-              f"{r['instance_ms']:8.3f}  {r['bound_ms']:5.3f}  {r['slowest_ms']:7.3f}  {r['mean_ms']:5.3f}")
+        print(f"{r['step']:4d}  {r['kernel_ms'] or float('nan'):6.3f}  {r['ranked_ms']:6.3f}  {r['prevtime_ms']:8.3f}  "
+              f"{r['ideal_ms']:5.3f}  "
+              f"{r['instance_ms']:8.3f}  {r['xcd_ms']:5.3f}  {r['bound_ms']:5.3f}  {r['slowest_ms']:7.3f}  {r['mean_ms']:5.3f}")
     mean = {k: float(np.mean([r[k] for r in rows])) for k in rows[0] if k != "step"}
     print("mean  " + "  ".join(f"{k} {v:.3f}" for k, v in mean.items()))
     print(json.dumps({"config": vars(args), "slots": slots, "mean": mean, "steps": rows}))
