@@ -57,6 +57,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--slots", type=int, default=0, help="workgroups resident at once (0: one per CU)")
+    ap.add_argument("--tail-work", type=float, default=0.0,
+                    help="ms of extra work appended to every instance but the K last finishers: prints how far "
+                         "it would extend the step's slowest instance for K = B/8, B/4, B/2 (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -120,7 +123,14 @@ def main():
                          "instance_ms": makespan(times, np.arange(B), slots),
                          "xcd_ms": makespan(times, ranked, slots, 8),
                          "bound_ms": max(times.max(), times.sum() / slots), "slowest_ms": float(times.max()),
-                         "mean_ms": float(times.mean())})
+                         "mean_ms": float(times.mean()),
+                         "p50_ms": float(np.percentile(times, 50)), "p75_ms": float(np.percentile(times, 75)),
+                         "p90_ms": float(np.percentile(times, 90))})
+            if args.tail_work > 0:
+                srt = np.sort(times)
+                for frac in (8, 4, 2):
+                    K = B // frac
+                    rows[-1][f"ext_k{K}_ms"] = float(max(0.0, srt[B - K - 1] + args.tail_work - srt[-1]))
         prev_cost, prev_times = cost.astype(np.float64), times.copy()
     print("step  kernel  ranked  prevtime  ideal  instance  xcd  bound  slowest  mean   (ms; schedules of the "
           "measured instance times)")
