@@ -8,4 +8,4 @@ timeout -k 10 200 python3 -u tools/phase_timing.py --batch 1024 --warmup 5 --ste
 timeout -k 10 200 python3 -u tools/phase_timing.py --batch 128 --warmup 5 --steps 20 > "$OUT/phase_b128.txt" 2>&1 || exit $?
 timeout -k 10 300 python3 -u tools/phase_timing.py --model quad3d --batch 512 --n-train 4000 --fitc 2000 --horizon 40 \
     --var-inputs dynamics --warmup 5 --steps 20 > "$OUT/phase_config5.txt" 2>&1 || exit $?
-tail -16 "$OUT"/phase_b1024.txt "$OUT"/phase_b128.txt
+tail -n 16 "$OUT"/phase_b1024.txt "$OUT"/phase_b128.txt
