@@ -27,8 +27,7 @@
 #include "gpmpc_common.h"
 #include "models.h"
 
-#ifndef GPMPC_SEG_FALLBACK   // 1: boundary-chain pivot check and one-segment fallback (A/B variants: 0 neither,
-                             // 2 the check and its flag without the fallback, 3 the fallback without the check)
+#ifndef GPMPC_SEG_FALLBACK   // 1: boundary-chain pivot check and one-segment fallback (A/B variants: 0)
 #define GPMPC_SEG_FALLBACK 1
 #endif
 #ifndef GPMPC_SOLVE_STAMP    // 1: per-instance solve time in stats slots 10-11 (A/B variants: 0)
@@ -2052,7 +2051,7 @@ struct SqpKernel {
                 double cp[NX];
 #pragma unroll
                 for (int i = 0; i < NX; ++i) cp[i] = readlane_d(col[i], p);
-                piv_ok = piv_ok && (GPMPC_SEG_FALLBACK == 3 || cp[p] > pmin);   // (false for a NaN pivot too)
+                piv_ok = piv_ok && (cp[p] > pmin);   // (false for a NaN pivot too)
                 const double inv = fast_rcp(cp[p]);
                 col[p] *= inv;
 #pragma unroll
@@ -2314,15 +2313,14 @@ struct SqpKernel {
     //   kCmdSegVector (corrector): B1 | vector passes | Bm1 | wave 1: chain, others: affine columns |
     //                 Bm2 | forward | B2
     // Factorisation statuses in ctrl[8 + w].  Fallback: when the boundary chain meets a pivot it cannot
-    // trust (seg_chain_full), it sets ctrl[kFb]; every wave reads the flag after Bm2 but the segments'
-    // fold and sweep run regardless, and after B2 the chain wave runs the one-segment recursion over the
-    // whole horizon in the same layout (factorisation into ctrl[kFb + 1], closed-loop maps, forward
-    // sweep from dx_0 = 0), overwriting what they wrote, before an extra barrier B3; the corrector of
-    // the same IPM iteration likewise runs its one-segment vector pass, maps and sweep after its B2.
-    // Same barriers on every wave (the flag is the workgroup's).  Reading the flag only where the
-    // common path does not wait on it keeps the fallback's cost off that path (a flag tested before
-    // the sweeps cost the 4- and 8-GPU shards 3 %, profiles/r6/ab_fallback/).
-    static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4;
+    // trust (seg_chain_full), it sets ctrl[kFb]; the segments' fold and sweep run regardless, and wave 0
+    // (which reads the flag after Bm2, where it has slack) then posts a fallback command after B2: the
+    // chain wave runs the one-segment recursion over the whole horizon in the same layout
+    // (seg_fallback: factorisation into ctrl[kFb + 1], closed-loop maps, forward sweep from dx_0 = 0),
+    // overwriting what the segments wrote; the corrector of the same IPM iteration likewise.  The helper
+    // waves never read the flag (a flag tested by every wave before the sweeps cost the 4- and 8-GPU
+    // shards 3 %, one tested after B2 1.5 %, profiles/r6/ab_fallback/).
+    static constexpr int kCmdSegFactor = -3, kCmdSegVector = -4, kCmdSegFbFactor = -5, kCmdSegFbVector = -6;
     static constexpr int kFb = 12;   // ctrl slots: fallback flag, fallback factorisation status
     static constexpr int kTs = 14;   // ctrl slots 14-15: the instance's start time stamp (stats slot 10)
     __host__ __device__ static constexpr int seg_of_wave(int w) { return NSEG == 3 ? w - 1 : (w == 1 ? 0 : (w == 0 ? 1 : -1)); }
@@ -2340,7 +2338,7 @@ struct SqpKernel {
         }
     }
     template <int KIND>
-    __device__ static bool seg_part(const Lds& L, int H, int lane, int w, int sg, bool chain, int cmd) {
+    __device__ static bool seg_part(const Lds& L, int H, int lane, int w, int sg, bool chain, int cmd, int* fb = nullptr) {
         const int k0 = seg_start(sg, H), k1 = seg_start(sg + 1, H);
         double* xs = L.sb + SB_XM + 8 * sg;
         int a0, a1;
@@ -2372,10 +2370,7 @@ struct SqpKernel {
             }
             if (a1 > a0) seg_acl<true>(L, lane, a0, a1);
             __syncthreads();   // Bm2: lambda_b, x_w, A'_k
-            // (the fallback flag is read here and used after B2: the segments' fold and sweep run
-            // whatever it says, and a fallback overwrites what they wrote, so the common path never
-            // waits on the flag's LDS round trip)
-            const int fbf = GPMPC_SEG_FALLBACK != 0 ? L.ctrl[kFb] : 0;
+            if (fb != nullptr) *fb = L.ctrl[kFb];   // (wave 0: read here, used after B2 by seg_run)
             if (ok) {
                 if constexpr (KIND == 1) {
                     seg_fold(L, lane, k0, k1, L.sb + SB_LAM + 8 * sg);
@@ -2386,24 +2381,8 @@ struct SqpKernel {
                 }
             }
             __syncthreads();   // B2
-            if ((GPMPC_SEG_FALLBACK & 1) && ok && fbf != 0) {   // (uniform over the workgroup: every wave read the flag)
-                if (chain) {   // the one-segment recursion instead (Ph singular at a boundary)
-                    const bool fok = seg_factor<false>(L, H, lane, 0, H, nullptr);
-                    if (lane == 0) L.ctrl[kFb + 1] = fok ? 1 : 0;
-                    WSYNC();
-                    if (fok) {
-                        seg_acl<true>(L, lane, 0, H);
-                        WSYNC();
-                        seg_forward(L, lane, 0, H, nullptr, true);
-                    }
-                }
-                __syncthreads();   // B3 (fallback only)
-                ok = L.ctrl[kFb + 1] != 0;
-            }
         } else {
-            // (this IPM iteration's predictor set the flag; as there, the segments' passes run whatever
-            // it says and a fallback overwrites their results after B2)
-            const int fbf = GPMPC_SEG_FALLBACK != 0 ? L.ctrl[kFb] : 0;
+            if (fb != nullptr) *fb = L.ctrl[kFb];   // (this IPM iteration's predictor set it)
             if constexpr (KIND == 1) seg_vector_backward(L, H, lane, k0, k1, false, L.sb + SB_VL1 + 8 * sg);
             if constexpr (KIND == 2) seg_vector_backward(L, H, lane, k0, H, true, nullptr);
             __syncthreads();   // Bm1
@@ -2418,24 +2397,49 @@ struct SqpKernel {
                 seg_forward(L, lane, k0, H, xs, true);
             }
             __syncthreads();   // B2
-            if ((GPMPC_SEG_FALLBACK & 1) && fbf != 0) {
-                if (chain) {
-                    seg_vector_backward(L, H, lane, 0, H, true, nullptr);
-                    seg_acl<false>(L, lane, 0, H);
-                    WSYNC();
-                    seg_forward(L, lane, 0, H, nullptr, true);
-                }
-                __syncthreads();   // B3 (fallback only)
-            }
         }
         return ok;
     }
-    // wave 0 (inside qp_ipm): post the command, then its own part
+    // The chain wave's one-segment recursion over the whole horizon in the segment layout (the fallback
+    // commands): predictor -- factorisation (status into ctrl[kFb + 1]), closed-loop maps, forward sweep
+    // from dx_0 = 0; corrector -- vector pass, affine columns, forward sweep.  It overwrites everything
+    // the segments' fold and sweep wrote.
+    __device__ static void seg_fallback(const Lds& L, int H, int lane, int cmd) {
+        if (cmd == kCmdSegFbFactor) {
+            const bool fok = seg_factor<false>(L, H, lane, 0, H, nullptr);
+            if (lane == 0) L.ctrl[kFb + 1] = fok ? 1 : 0;
+            WSYNC();
+            if (fok) {
+                seg_acl<true>(L, lane, 0, H);
+                WSYNC();
+                seg_forward(L, lane, 0, H, nullptr, true);
+            }
+        } else {
+            seg_vector_backward(L, H, lane, 0, H, true, nullptr);
+            seg_acl<false>(L, lane, 0, H);
+            WSYNC();
+            seg_forward(L, lane, 0, H, nullptr, true);
+        }
+    }
+    // wave 0 (inside qp_ipm): post the command, then its own part; when the chain refused a pivot, one
+    // more command has the chain wave redo the solve as the one-segment recursion (B1 | recursion | B2),
+    // so the helper waves never wait on the flag
     __device__ static bool seg_run(const Lds& L, int H, int lane, int cmd) {
         if (lane == 0) L.ctrl[0] = cmd;
         __syncthreads();   // B1
         constexpr int sg0 = seg_of_wave(0);
-        return seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd);
+        int fbv = 0;
+        bool ok = seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd, &fbv);
+        if constexpr (GPMPC_SEG_FALLBACK) {
+            if (ok && fbv != 0) {
+                const bool pred = cmd == kCmdSegFactor;
+                if (lane == 0) L.ctrl[0] = pred ? kCmdSegFbFactor : kCmdSegFbVector;
+                __syncthreads();   // B1
+                __syncthreads();   // B2 (the chain wave's recursion)
+                if (pred) ok = L.ctrl[kFb + 1] != 0;
+            }
+        }
+        return ok;
     }
     // helper wave w's part of a segment command (after B1)
     __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
@@ -2948,6 +2952,11 @@ struct SqpKernel {
             if constexpr (kSeg) {   // a segment-parallel Newton solve (seg_run)
                 if (G == kCmdSegFactor || G == kCmdSegVector) {
                     seg_helper(L, H, lane, w, G);
+                    continue;
+                }
+                if (G == kCmdSegFbFactor || G == kCmdSegFbVector) {   // (the chain wave: w = 1)
+                    if (w == 1) seg_fallback(L, H, lane, G);
+                    __syncthreads();   // B2
                     continue;
                 }
             }
