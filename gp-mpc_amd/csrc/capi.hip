@@ -312,6 +312,7 @@ gpmpc_status gpmpc_create(int32_t model_id, int32_t horizon, int32_t max_batch, 
     P.waves = 0;            // automatic launch shape (gpmpc_set_launch)
     P.order_dispatch = 1;   // cost-ordered dispatch of multi-round launches (GPMPC_TUNE_ORDER)
     P.seg = 1;              // segment-parallel Newton solves (GPMPC_TUNE_SEG)
+    P.seg_piv_rel = 1e-10;  // their boundary chain's pivot threshold (GPMPC_TUNE_SEG_PIVOT)
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) ncu = 0;
@@ -923,6 +924,11 @@ gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value) {
         case GPMPC_TUNE_SEG:
             if (value != 0 && value != 1) break;
             h->P.seg = value;
+            return GPMPC_OK;
+        case GPMPC_TUNE_SEG_PIVOT:
+            // threshold 10^-value; -1: every pivot refused (every solve takes the fallback, a test of it)
+            if (value < -1 || value > 300) break;
+            h->P.seg_piv_rel = value < 0 ? HUGE_VAL : std::pow(10.0, -value);
             return GPMPC_OK;
         case GPMPC_TUNE_TAIL:
             if (value < -1 || value > 16384) break;

@@ -88,6 +88,9 @@ struct ProblemDev {
     // segment-parallel Newton solves when the launch runs two or four waves per instance (single-tile
     // models; gpmpc_set_tuning GPMPC_TUNE_SEG)
     int32_t seg;
+    // the boundary chain's pivot threshold relative to Ph's largest diagonal entry (gpmpc_set_tuning
+    // GPMPC_TUNE_SEG_PIVOT): below it the solve falls back to the one-segment recursion
+    double seg_piv_rel;
     GPDev gp[kMaxGP];
 };
 

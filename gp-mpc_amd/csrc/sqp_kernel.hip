@@ -1995,11 +1995,11 @@ struct SqpKernel {
     // M is positive definite only while Ph is: a state direction that no cost, bound barrier or
     // coupling reaches (q_i = 0 on an unbounded or barely bounded state) leaves Ph singular and a
     // pivot at rounding level.  Every pivot is checked against the largest diagonal entry of Ph
-    // (kPivRel; M = Ph (I + W Ph) with W >= 0 has no smaller diagonal, and Ph is in every lane's
+    // (ProblemDev::seg_piv_rel, 1e-10 by default; M = Ph (I + W Ph) with W >= 0 has no smaller
+    // diagonal, and Ph is in every lane's
     // registers already, so the check adds no cross-lane move to the chain): the return value false
     // sends the solve to the one-segment recursion (seg_part's fallback), which never inverts Ph.
-    static constexpr double kPivRel = 1e-10;
-    __device__ static bool seg_chain_full(const Lds& L, int H, int lane) {
+    __device__ static bool seg_chain_full(const Lds& L, int H, int lane, double P_piv_rel) {
         lane = phase_lane(lane);
         constexpr int CI = NX;
         const int c = min(lane, 3 * NX);
@@ -2045,7 +2045,7 @@ struct SqpKernel {
             double dmx = 0.0;   // largest diagonal entry of Ph
 #pragma unroll
             for (int i = 0; i < NX; ++i) dmx = fmax(dmx, pk[pidx(i, i)]);
-            const double pmin = kPivRel * dmx;
+            const double pmin = P_piv_rel * dmx;
 #pragma unroll
             for (int p = 0; p < NX; ++p) {
                 double cp[NX];
@@ -2338,7 +2338,8 @@ struct SqpKernel {
         }
     }
     template <int KIND>
-    __device__ static bool seg_part(const Lds& L, int H, int lane, int w, int sg, bool chain, int cmd, int* fb = nullptr) {
+    __device__ static bool seg_part(const Lds& L, int H, int lane, int w, int sg, bool chain, int cmd, double piv_rel,
+                                    int* fb = nullptr) {
         const int k0 = seg_start(sg, H), k1 = seg_start(sg + 1, H);
         double* xs = L.sb + SB_XM + 8 * sg;
         int a0, a1;
@@ -2363,7 +2364,7 @@ struct SqpKernel {
                 ok = all != 0;
             }
             if (chain && ok) {
-                const bool cok = seg_chain_full(L, H, lane);
+                const bool cok = seg_chain_full(L, H, lane, piv_rel);
                 if constexpr (GPMPC_SEG_FALLBACK) {
                     if (lane == 0) L.ctrl[kFb] = cok ? 0 : 1;
                 }
@@ -2429,7 +2430,7 @@ struct SqpKernel {
         __syncthreads();   // B1
         constexpr int sg0 = seg_of_wave(0);
         int fbv = 0;
-        bool ok = seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd, &fbv);
+        bool ok = seg_part<sg0 < 0 ? 0 : (sg0 == NSEG - 1 ? 2 : 1)>(L, H, lane, 0, sg0 < 0 ? 0 : sg0, false, cmd, 0.0, &fbv);
         if constexpr (GPMPC_SEG_FALLBACK) {
             if (ok && fbv != 0) {
                 const bool pred = cmd == kCmdSegFactor;
@@ -2442,11 +2443,11 @@ struct SqpKernel {
         return ok;
     }
     // helper wave w's part of a segment command (after B1)
-    __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd) {
+    __device__ static void seg_helper(const Lds& L, int H, int lane, int w, int cmd, double piv_rel) {
         const int sg = seg_of_wave(w);
-        if (sg == NSEG - 1) (void)seg_part<2>(L, H, lane, w, sg, w == 1, cmd);
-        else if (sg >= 0) (void)seg_part<1>(L, H, lane, w, sg, w == 1, cmd);
-        else (void)seg_part<0>(L, H, lane, w, 0, false, cmd);
+        if (sg == NSEG - 1) (void)seg_part<2>(L, H, lane, w, sg, w == 1, cmd, piv_rel);
+        else if (sg >= 0) (void)seg_part<1>(L, H, lane, w, sg, w == 1, cmd, piv_rel);
+        else (void)seg_part<0>(L, H, lane, w, 0, false, cmd, piv_rel);
     }
 
     // C' pi restricted to stage k variables: x_k: pi_{k-1} - A_k' pi_k ; u_k: -B_k' pi_k.
@@ -2951,7 +2952,7 @@ struct SqpKernel {
             if (G == -1) break;
             if constexpr (kSeg) {   // a segment-parallel Newton solve (seg_run)
                 if (G == kCmdSegFactor || G == kCmdSegVector) {
-                    seg_helper(L, H, lane, w, G);
+                    seg_helper(L, H, lane, w, G, P.seg_piv_rel);
                     continue;
                 }
                 if (G == kCmdSegFbFactor || G == kCmdSegFbVector) {   // (the chain wave: w = 1)

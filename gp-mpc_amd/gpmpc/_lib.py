@@ -65,7 +65,7 @@ SIGNATURES = {
 }
 
 # gpmpc_set_tuning options (include/gpmpc_mi355x.h GPMPC_TUNE_*)
-TUNE = {"lin_cache": 0, "order": 1, "overlap": 2, "var_split": 3, "event_fence": 4, "seg": 5, "tail": 6}
+TUNE = {"lin_cache": 0, "order": 1, "overlap": 2, "var_split": 3, "event_fence": 4, "seg": 5, "tail": 6, "seg_pivot": 7}
 
 
 class GPMPCError(RuntimeError):

@@ -214,7 +214,7 @@ class BatchSolver:
 
     def set_tuning(self, **opts):
         """Performance switches (gpmpc_set_tuning): lin_cache=0/1, order=0/1/2, overlap=0/1,
-        var_split=0/1/4, event_fence=0/1, seg=0/1, tail=K.  Outputs do not depend on them (A/B knobs)."""
+        var_split=0/1/4, event_fence=0/1, seg=0/1, tail=K, seg_pivot=k.  Outputs do not depend on them (A/B knobs)."""
         for k, v in opts.items():
             if k not in _lib.TUNE:
                 raise ValueError(f"unknown tuning option {k!r} (one of {sorted(_lib.TUNE)})")

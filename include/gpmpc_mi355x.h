@@ -233,7 +233,11 @@ gpmpc_status gpmpc_get_launch_segments(gpmpc_handle* h, int32_t batch, int32_t* 
  *                          instances (by the cost of their previous solve) as two-wave segment solves
  *                          on the caller's stream, beside the other instances' one-wave launch on a
  *                          second stream; identical up to rounding (each instance's arithmetic is that of
- *                          its launch shape).  The SQP profiling events then bracket both launches */
+ *                          its launch shape).  The SQP profiling events then bracket both launches
+ *   GPMPC_TUNE_SEG_PIVOT   10 (default): the segment solve's boundary chain refuses a pivot below
+ *                          10^-value x Ph's largest diagonal entry and redoes that Newton solve as
+ *                          the one-segment recursion; -1: refuses every pivot (every segment solve
+ *                          takes that fallback: a test of it) */
 enum {
     GPMPC_TUNE_LIN_CACHE = 0,
     GPMPC_TUNE_ORDER = 1,
@@ -241,7 +245,8 @@ enum {
     GPMPC_TUNE_VAR_SPLIT = 3,
     GPMPC_TUNE_EVENT_FENCE = 4,
     GPMPC_TUNE_SEG = 5,
-    GPMPC_TUNE_TAIL = 6
+    GPMPC_TUNE_TAIL = 6,
+    GPMPC_TUNE_SEG_PIVOT = 7
 };
 gpmpc_status gpmpc_set_tuning(gpmpc_handle* h, int32_t option, int32_t value);
 

@@ -185,9 +185,10 @@ def test_segment_solve_with_an_unweighted_free_state():
     """Advisor finding (round 5): the boundary chain inverts M = Ph + Ph W Ph without pivoting, which
     needs the cost-to-go Ph at the boundary to be positive definite.  With q = 0 on the x position and
     its bounds at +-1e3 no cost or bound barrier reaches that direction (the position feeds no other
-    state), so Ph is singular up to rounding there.  The chain's pivot check (seg_chain_full, kPivRel)
-    must send such a solve to the one-segment recursion: same status and solution as the launch shape
-    without segments."""
+    state), so Ph is singular up to rounding there.  Same status and solution as the launch shape
+    without segments.  (The tiny pivot sits in a direction no other state couples to, so this case also
+    passes with the pivot check compiled out, profiles/r6/final_check/; the forced-fallback test below is
+    the one that runs the fallback.)"""
     spec, data, hyp = problem("quad2d", 60)
     mats = lqr(spec)   # the tightening's LQR gain from the weighted problem
     spec.q_diag[0] = 0.0
@@ -196,7 +197,20 @@ def test_segment_solve_with_an_unweighted_free_state():
         _seg_vs_one_segment(spec, data, hyp, mats, 30, waves)
 
 
-def _seg_vs_one_segment(spec, data, hyp, mats, H, waves):
+@pytest.mark.parametrize("waves", [2, 4])
+@pytest.mark.parametrize("name,N,H", [("quad2d", 200, 30), ("quad2d", 60, 5), ("cartpole", 40, 11)])
+def test_segment_fallback_matches_one_segment_recursion(name, N, H, waves):
+    """The boundary chain's fallback (seg_fallback: the chain wave redoes the Newton solve as the
+    one-segment recursion in the segment layout, after the segments' own fold and sweep) on every
+    predictor and corrector: GPMPC_TUNE_SEG_PIVOT = -1 refuses every pivot.  Same closed loop as the
+    launch shape without segments: identical status, x and u within 1e-6 (1 + |.|).  (The unweighted
+    free state above also passes with the check compiled out -- its tiny pivot sits in a decoupled
+    direction -- so this is the test that runs the fallback.)"""
+    spec, data, hyp = problem(name, N)
+    _seg_vs_one_segment(spec, data, hyp, lqr(spec), H, waves, seg_pivot=-1)
+
+
+def _seg_vs_one_segment(spec, data, hyp, mats, H, waves, seg_pivot=None):
     torch = _torch()
     from gpmpc.solver import BatchSolver
 
@@ -206,6 +220,8 @@ def _seg_vs_one_segment(spec, data, hyp, mats, H, waves):
         gs = BatchSolver(spec, H, B, tol=1e-9, qp_tol=1e-11, qp_max_iter=100)
         gs.set_launch(waves=waves)
         gs.set_tuning(seg=seg)
+        if seg and seg_pivot is not None:
+            gs.set_tuning(seg_pivot=seg_pivot)
         gs.set_gps(product_gps(data, hyp))
         gs.set_tightening(True, 0.95, *mats)
         gs.reset(reset_iterate=True)
